@@ -1,0 +1,125 @@
+/* sa_hip.h — C ABI of the MI355X (gfx950) alignment engine: the drop-in boundary for the
+ * reference's GPU path.
+ *
+ * The reference exposes exactly one GPU entry point,
+ *     uint64_t SequenceAlignment::alignSequenceGPU(const Request&, Response*);
+ *         (robertszafa/sequence-alignment-gpu: SequenceAlignment.hpp:127, implemented in
+ *          alignSequenceGPU.cu:463-653)
+ * with C++ linkage and C++ structs. This header is the plain-C layer underneath our C++14
+ * re-implementation of that function (sequence-alignment-gpu_amd/csrc/host/align_gpu.cpp):
+ * plain pointers and sizes, no torch / HIP types in the signatures, so any FFI (ctypes, cgo,
+ * JNI, N-API) can bind it. INTEGRATION.md shows the bindings.
+ *
+ * Semantics are those of the reference's CPU path (alignSequenceCPU.cpp:10-333), bit-exact:
+ * score, aligned text, aligned pattern, start indices — including the local-alignment
+ * start-index quirk and the "first maximum in row-major order" rule.
+ *
+ * Error behaviour mirrors the reference boundary: every entry point returns SA_OK (0) on
+ * success and a non-zero code otherwise (the reference returns 1 on failure,
+ * alignSequenceGPU.cu:543-545, :590-593); sa_last_error() gives the message.
+ */
+#ifndef SA_HIP_H
+#define SA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_ABI_VERSION 1
+
+/* Request::alignmentType (SequenceAlignment.hpp:78; GLOBAL/LOCAL of programArgs :17). */
+enum sa_mode { SA_GLOBAL = 0, SA_LOCAL = 1 };
+
+enum sa_status {
+    SA_OK = 0,
+    SA_ERR_INVALID = 1,     /* bad argument (sizes, alphabet, score range)                  */
+    SA_ERR_NOMEM = 2,       /* device allocation failed (reference: MEM_ERROR, :543)       */
+    SA_ERR_HIP = 3,         /* a HIP runtime call failed                                    */
+    SA_ERR_UNSUPPORTED = 4, /* input outside the engine's documented limits                 */
+    SA_ERR_TIMEOUT = 5      /* an in-kernel hand-off did not complete (engine aborted)      */
+};
+
+/* Scoring scheme of a Request (SequenceAlignment.hpp:71-99). */
+typedef struct sa_params {
+    int32_t mode;                 /* SA_GLOBAL (Needleman-Wunsch) or SA_LOCAL (Smith-Waterman)  */
+    int32_t alphabet_size;        /* Request::alphabetSize, 1..32 (4 DNA, 23 protein)           */
+    int32_t gap_penalty;          /* Request::gapPenalty (linear gap, subtracted per gap cell)  */
+    int32_t rows_per_lane;        /* 0 = automatic; else 1,2,4,8,16,32 (tuning knob)            */
+    const int32_t *score_matrix;  /* host, alphabet_size^2 ints, row-major [pattern][text]
+                                     (Request::scoreMatrix, indexed as alignSequenceCPU.cpp:172) */
+    const char *alphabet;         /* host, alphabet_size letters followed by the gap letter
+                                     (Request::alphabet; DNA_ALPHABET / PROTEIN_ALPHABET :56-58) */
+} sa_params;
+
+/* One (text, pattern) pair inside device-resident arenas of alphabet indices. */
+typedef struct sa_pair {
+    uint64_t text_offset;     /* byte offset of the text in the text arena        */
+    uint64_t text_len;        /* Request::textNumBytes    (columns of the DP)     */
+    uint64_t pattern_offset;  /* byte offset of the pattern in the pattern arena  */
+    uint64_t pattern_len;     /* Request::patternNumBytes (rows of the DP)        */
+} sa_pair;
+
+/* Per-pair outcome: the scalar fields of Response (SequenceAlignment.hpp:101-120). */
+typedef struct sa_result {
+    int32_t score;                 /* Response::score                                     */
+    int32_t status;                /* SA_OK or an error code for this pair               */
+    uint64_t num_alignment_bytes;  /* Response::numAlignmentBytes                         */
+    uint64_t start_text;           /* Response::startInAlignedText    (may be (uint64)-1) */
+    uint64_t start_pattern;        /* Response::startInAlignedPattern (may be (uint64)-1) */
+} sa_result;
+
+typedef struct sa_plan sa_plan;
+
+/* ---- one-shot, host pointers (what alignSequenceGPU needs) ------------------------------ */
+
+/* Align one pair held in host memory (alphabet indices). Synchronous. aligned_text and
+ * aligned_pattern receive num_alignment_bytes letters in forward order; cap must be at least
+ * text_len + pattern_len. If fill_us is non-NULL it receives the device time of the DP fill in
+ * microseconds (the quantity the reference returns under -DBENCHMARK, alignSequenceGPU.cu:613-626). */
+int sa_align_pair(const sa_params *params, const char *text, uint64_t text_len,
+                  const char *pattern, uint64_t pattern_len, int device, sa_result *out,
+                  char *aligned_text, char *aligned_pattern, uint64_t cap, double *fill_us);
+
+/* ---- plans: many pairs, device-resident inputs, explicit stream ------------------------- */
+
+/* Build a plan (strip layout, workspace) for num_pairs pairs on `device`. Allocates all device
+ * workspace once; the plan can be filled/traced back any number of times. */
+int sa_plan_create(const sa_params *params, const sa_pair *pairs, int64_t num_pairs, int device,
+                   sa_plan **out);
+int sa_plan_destroy(sa_plan *plan);
+
+/* Enqueue the DP fill of every pair on `stream` (a hipStream_t; NULL = the plan's own stream).
+ * d_text / d_pattern are device arenas of alphabet indices addressed by sa_pair offsets. */
+int sa_plan_fill(sa_plan *plan, const void *d_text, const void *d_pattern, void *stream);
+
+/* Enqueue the traceback of every pair (after sa_plan_fill on the same stream). */
+int sa_plan_traceback(sa_plan *plan, void *stream);
+
+/* Synchronise `stream` and copy the per-pair results to host (num_pairs entries). Returns
+ * SA_ERR_TIMEOUT if the fill aborted. */
+int sa_plan_fetch_results(sa_plan *plan, sa_result *out, void *stream);
+
+/* Synchronise `stream` and copy pair `index`'s aligned strings (forward order) to host. */
+int sa_plan_fetch_alignment(sa_plan *plan, int64_t index, char *aligned_text, char *aligned_pattern,
+                            uint64_t cap, void *stream);
+
+/* Introspection for benches and tests. */
+int sa_plan_info(const sa_plan *plan, int64_t *num_strips, int32_t *rows_per_lane,
+                 uint64_t *device_bytes, uint64_t *mask_bytes);
+/* Device pointer to the per-pair sa_result array written by sa_plan_traceback. */
+const void *sa_plan_device_results(const sa_plan *plan);
+
+/* ---- misc ------------------------------------------------------------------------------ */
+int sa_device_count(int *count);
+const char *sa_last_error(void);
+int sa_abi_version(void);
+/* Runs the engine's wave-level primitive self-test on `device` (DPP lane shifts, ballots);
+ * returns SA_OK when the hardware behaves as the kernels assume. */
+int sa_selftest(int device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SA_HIP_H */

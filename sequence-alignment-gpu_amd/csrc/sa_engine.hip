@@ -1,0 +1,1121 @@
+// MI355X (gfx950 / CDNA4) alignment engine: Needleman-Wunsch / Smith-Waterman DP fill and traceback.
+//
+// Replaces the reference's GPU path (robertszafa/sequence-alignment-gpu alignSequenceGPU.cu:73-653)
+// with a new design; see DESIGN.md and sa_layout.h for the data layout. Semantics follow the
+// reference CPU path (alignSequenceCPU.cpp), bit-exact:
+//   cell recurrence and tie rule      alignSequenceCPU.cpp:175-190 (local), :259-273 (global)
+//   boundaries                        :145-149, :163-164 (local), :232-236, :247-248 (global)
+//   local best cell (first max)       :191-192
+//   tracebacks                        traceBackNW :64-114, traceBackSW :10-62
+//
+// Fill kernel (one wave64 per strip, dynamic strip queue):
+//   * lane k owns R rows and works on column s-k+1 at step s; the value from the row above
+//     arrives by a DPP wave_shr:1 lane shift, lane 0 is fed from the strip above (granules);
+//   * the substitution score comes from a per-row profile register (DNA: four int8 scores packed
+//     in one VGPR, selected by v_bfe_i32 on the text code) or from an LDS table (protein);
+//   * global alignment runs in the shifted domain F = H + g*(i+j), where the recurrence
+//     becomes F = max(Fdiag + s + 2g, Fleft, Fup) and every boundary is 0;
+//   * the direction of each cell is never materialised per lane: two wave ballots per
+//     (step,row) are the two bit-planes of the DIRECTION code, collected with v_writelane into
+//     one VGPR per 16 (step,row) slots and written as coalesced 256-byte stores.
+// Traceback kernel (one wave per pair): walks the bit-planes through an LDS window, then
+// converts the op string to letters in parallel.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "sa_hip.h"
+#include "sa_layout.h"
+
+namespace sa {
+
+// ------------------------------------------------------------------------------------------------
+// wave-level helpers
+// ------------------------------------------------------------------------------------------------
+template <typename F, int... Is>
+__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, Is...>)
+{
+    (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F &&f)
+{
+    sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// DPP lane moves (GFX9 wavefront shifts). wave_shr:1 — lane i reads lane i-1, lane 0 keeps `old`;
+// wave_shl:1 — lane i reads lane i+1, lane 63 keeps `old`; wave_rol:1 — lane i reads lane i+1 mod 64.
+__device__ __forceinline__ int dpp_shr1(int old, int src) { return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ int dpp_shl1(int old, int src) { return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false); }
+__device__ __forceinline__ int dpp_rol1(int src) { return __builtin_amdgcn_update_dpp(src, src, 0x134, 0xf, 0xf, false); }
+
+template <int L>
+__device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
+{
+    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(acc) : "s"(v), "i"(L));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
+{
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64);
+    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+__device__ __forceinline__ uint64_t load_granule(const uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store_granule(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------------
+// fill kernel
+// ------------------------------------------------------------------------------------------------
+template <int R>
+struct Cfg {
+    static constexpr int U = (16 / R) > 4 ? (16 / R) : 4;  // steps per unrolled body
+    static constexpr int SLOTS = U * R;                     // (step,row) slots per body
+    static constexpr int NACC = SLOTS / 16;                 // direction accumulators (VGPRs)
+    static_assert(SLOTS % 16 == 0, "body must fill whole accumulators");
+};
+
+struct FillArgs {
+    const int8_t *pattern;      // device pattern arena (alphabet indices)
+    const int8_t *codes;        // padded text codes (8*c for the packed profile, c otherwise)
+    const StripDesc *strips;
+    const PairDesc *pairs;
+    const int32_t *prof_tab;    // packed profile: one word per pattern letter (A <= 4)
+    const int32_t *score_tab;   // generic: A*A scores (+2g for global)
+    uint32_t *masks;            // direction entries, viewed as dwords
+    uint64_t *bnd;              // hand-off granules
+    uint64_t *strip_best;       // local: best-cell key per strip
+    int32_t *pair_score;        // global: H[m][n] per pair
+    Control *ctrl;
+    int32_t num_strips;
+    int32_t gap;
+    int32_t A;
+    uint32_t epoch;
+    int32_t key_bits;
+};
+
+// Waits until lanes 0..U-1 hold the granules of columns base+1 .. base+U of the strip above.
+// `v` is a value already loaded (prefetched); returns false if the launch is being aborted.
+template <int U>
+__device__ __forceinline__ bool wait_feed(const FillArgs &a, const uint64_t *bin, int base, int n,
+                                          int lane, uint64_t &v)
+{
+    const bool need = lane < U && base + lane < n;
+    bool ready = !need || (uint32_t)(v >> 32) == a.epoch;
+    if (__all(ready)) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 0;; ++spin)
+    {
+        __builtin_amdgcn_s_sleep(2);
+        if (!ready) v = load_granule(bin + base + lane);
+        ready = !need || (uint32_t)(v >> 32) == a.epoch;
+        if (__all(ready)) return true;
+        if ((spin & 63) == 63)
+        {
+            // 100 MHz constant clock: give up after ~20 s, and whenever another wave gave up.
+            const bool late = __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull;
+            if (late) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+        }
+    }
+}
+
+// One unrolled body of U steps. RAMP: some lanes are outside [1,n] and must keep their state.
+template <int R, bool LOCAL, bool PACKED, bool RAMP>
+__device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
+                                         int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
+                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &FB,
+                                         int &O, uint32_t (&acc)[Cfg<R>::NACC])
+{
+    constexpr int U = Cfg<R>::U;
+    sfor<U>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int s = s0 + q;
+        const int t = T[q];
+        // value of the row above this lane's first row, at this lane's column
+        int up = dpp_shr1(FB, F[R - 1]);
+        FB = dpp_rol1(FB);
+        int diag = upPrev;
+        upPrev = up;
+        int gu = up - g;  // local only
+        bool act = true;
+        if constexpr (RAMP)
+        {
+            const int c = s - lane;
+            act = (c >= 0) && (c < n);
+        }
+        const int kmask = (1 << kb) - 1;
+        const int Ks = kmask - (s & kmask);  // local: later column in a block = smaller key
+        sfor<R>([&](auto Rc) {
+            constexpr int rho = decltype(Rc)::value;
+            int sc;
+            if constexpr (PACKED) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
+            else sc = ldsS[prof[rho] + t];
+            uint64_t p0, p1;
+            if constexpr (!LOCAL)
+            {
+                const int left = F[rho];
+                const int D = diag + sc;
+                const int M = max(left, up);
+                int Fn = max(D, M);
+                const uint64_t d = ballot(D > M);
+                const uint64_t tp = ballot(up > left);
+                if constexpr (RAMP) Fn = act ? Fn : left;
+                diag = left;
+                up = Fn;
+                F[rho] = Fn;
+                p0 = d;
+                p1 = tp & ~d;
+            }
+            else
+            {
+                const int Hl = F[rho], Gl = G[rho];
+                const int D = diag + sc;
+                const int M = max(Gl, gu);
+                int Hn = max(max(D, M), 0);
+                const uint64_t d = ballot(D > M);
+                const uint64_t tp = ballot(gu > Gl);
+                const uint64_t z = ballot(Hn == 0);
+                int Gn = Hn - g;
+                const int key = (Hn << kb) + Ks;
+                if constexpr (RAMP)
+                {
+                    best[rho] = act ? max(best[rho], key) : best[rho];
+                    Hn = act ? Hn : Hl;
+                    Gn = act ? Gn : Gl;
+                }
+                else
+                {
+                    best[rho] = max(best[rho], key);
+                }
+                diag = Hl;
+                up = Hn;
+                gu = Gn;
+                F[rho] = Hn;
+                G[rho] = Gn;
+                p0 = d | z;
+                p1 = (tp & ~d) | z;
+            }
+            constexpr int slot = q * R + rho;
+            constexpr int ai = slot / 16, l = (slot % 16) * 4;
+            writelane<l + 0>(acc[ai], (uint32_t)p0);
+            writelane<l + 1>(acc[ai], (uint32_t)(p0 >> 32));
+            writelane<l + 2>(acc[ai], (uint32_t)p1);
+            writelane<l + 3>(acc[ai], (uint32_t)(p1 >> 32));
+        });
+        // collect the strip's bottom row: lane 63 appends, everything else moves down one lane
+        O = dpp_shl1(F[R - 1], O);
+    });
+}
+
+template <int R, bool LOCAL, bool PACKED>
+__device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, int idx, int lane)
+{
+    constexpr int U = Cfg<R>::U;
+    constexpr int NACC = Cfg<R>::NACC;
+    const StripDesc sd = a.strips[idx];
+    const PairDesc pd = a.pairs[sd.pair];
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
+    const int g = a.gap;
+    const int kb = a.key_bits;
+    const int rowTop = sd.row0 + lane * R;
+    int prof[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        const int i = rowTop + rho;
+        int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
+        c = min(max(c, 0), a.A - 1);
+        prof[rho] = PACKED ? a.prof_tab[c] : c * a.A;
+    });
+    const int8_t *codes = a.codes + pd.code_off + kPad;
+    const bool hasPrev = (sd.flags & kHasPrev) != 0;
+    const bool hasNext = (sd.flags & kHasNext) != 0;
+    const uint64_t *bin = a.bnd + sd.bnd_in;
+    uint64_t *bout = a.bnd + sd.bnd_out;
+    uint32_t *mk = a.masks + sd.mask_off * 4;
+    const int nSteps = sd.nsteps;
+
+    // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
+    int F[R], G[R], best[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        F[rho] = 0;
+        G[rho] = -g;
+        best[rho] = 0;
+    });
+    int upPrev = 0, FB = 0, O = 0;
+    int T[U], Tn[U];
+    sfor<U>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        T[q] = codes[q - lane];
+    });
+    bool ok = true;
+    if (hasPrev)
+    {
+        uint64_t v = (lane < U && lane < n) ? load_granule(bin + lane) : 0;
+        ok = wait_feed<U>(a, bin, 0, n, lane, v);
+        FB = (int)(uint32_t)v;
+    }
+    int published = 0;
+    uint64_t lbest = 0;
+    for (int s0 = 0; ok && s0 < nSteps; s0 += U)
+    {
+        const int s1 = s0 + U;
+        sfor<U>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            Tn[q] = codes[s1 + q - lane];
+        });
+        uint64_t gn = 0;
+        if (hasPrev && s1 < nSteps && lane < U && s1 + lane < n) gn = load_granule(bin + s1 + lane);
+        uint32_t acc[NACC];
+        sfor<NACC>([&](auto Cc) { acc[decltype(Cc)::value] = 0; });
+        const bool steady = (s0 >= kWave - 1) && (s1 <= n);
+        if (steady)
+            run_body<R, LOCAL, PACKED, false>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc);
+        else
+            run_body<R, LOCAL, PACKED, true>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc);
+        sfor<NACC>([&](auto Cc) {
+            constexpr int c = decltype(Cc)::value;
+            mk[((size_t)s0 * R + c * 16) * 4 + lane] = acc[c];
+        });
+        if (hasNext && (((s1 & 15) == 0) || s1 >= nSteps))
+        {
+            const int sl = s1 - 1;
+            const int col = sl - 125 + lane;  // column whose bottom value O holds in this lane
+            if (lane >= 48 && col >= 1 && col <= n && col > published)
+                store_granule(bout + col - 1, ((uint64_t)a.epoch << 32) | (uint32_t)O);
+            published = min(n, max(0, sl - 62));
+        }
+        if constexpr (LOCAL)
+        {
+            const int kmask = (1 << kb) - 1;
+            if (((s1 & kmask) == 0) || s1 >= nSteps)
+            {
+                const int blockBase = s0 & ~kmask;
+                sfor<R>([&](auto Rc) {
+                    constexpr int rho = decltype(Rc)::value;
+                    const int key = best[rho];
+                    const int H = key >> kb;
+                    const int st = blockBase + (kmask - (key & kmask));
+                    const int col = st - lane + 1;
+                    const int row = rowTop + rho;
+                    if (H > 0 && row <= m && col >= 1 && col <= n)
+                    {
+                        const uint64_t k64 = ((uint64_t)H << (2 * kKeyRowBits)) |
+                                             ((kKeyMask - (uint64_t)row) << kKeyRowBits) |
+                                             (kKeyMask - (uint64_t)col);
+                        lbest = max(lbest, k64);
+                    }
+                    best[rho] = 0;
+                });
+            }
+        }
+        if (hasPrev && s1 < nSteps)
+        {
+            ok = wait_feed<U>(a, bin, s1, n, lane, gn);
+            FB = (int)(uint32_t)gn;
+        }
+        sfor<U>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            T[q] = Tn[q];
+        });
+    }
+    if (!ok) return;
+    if constexpr (LOCAL)
+    {
+        for (int off = 32; off > 0; off >>= 1) lbest = max(lbest, shfl_xor_u64(lbest, off));
+        if (lane == 0) a.strip_best[idx] = lbest;
+    }
+    else
+    {
+        const int rm = m - sd.row0;  // strip-relative row of the last DP row
+        if (rm >= 0 && rm < kWave * R && lane == rm / R)
+        {
+            int v = F[0];
+            sfor<R>([&](auto Rc) {
+                constexpr int rho = decltype(Rc)::value;
+                if (rho == rm % R) v = F[rho];
+            });
+            a.pair_score[sd.pair] = v - g * (m + n);
+        }
+    }
+}
+
+template <int R, bool LOCAL, bool PACKED>
+__global__ __launch_bounds__(64) void fill_kernel(FillArgs a)
+{
+    __shared__ int ldsS[32 * 32];
+    const int lane = threadIdx.x;
+    if constexpr (!PACKED)
+    {
+        for (int e = lane; e < a.A * a.A; e += kWave) ldsS[e] = a.score_tab[e];
+        __syncthreads();
+    }
+    while (true)
+    {
+        uint32_t idx = 0;
+        if (lane == 0) idx = atomicAdd(&a.ctrl->queue_head, 1u);
+        idx = __shfl(idx, 0, 64);
+        if (idx >= (uint32_t)a.num_strips) break;
+        if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        process_strip<R, LOCAL, PACKED>(a, ldsS, (int)idx, lane);
+    }
+}
+
+__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int8_t *codes, int A, int scale)
+{
+    const PairDesc pd = pairs[blockIdx.y];
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
+         x += (uint64_t)gridDim.x * blockDim.x)
+    {
+        int c = text[pd.text_off + x];
+        c = min(max(c, 0), A - 1);
+        codes[pd.code_off + kPad + x] = (int8_t)(c * scale);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// traceback kernel
+// ------------------------------------------------------------------------------------------------
+constexpr int kWinEntries = 2048;  // 32 KiB LDS window of 16-byte direction entries
+
+struct TbArgs {
+    const int8_t *text, *pattern;
+    const StripDesc *strips;
+    const PairDesc *pairs;
+    const uint4 *masks;
+    const uint64_t *strip_best;
+    const int32_t *pair_score;
+    uint8_t *ops;
+    char *out_text, *out_pattern;
+    sa_result *results;
+    int32_t mode, gap, A;
+    char alphabet[33];
+};
+
+enum { kLeft = 0, kDiag = 1, kTop = 2, kStop = 3 };  // SequenceAlignment.hpp:122
+
+template <int R>
+__global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
+{
+    __shared__ uint4 win[kWinEntries];
+    __shared__ char alpha[40];
+    __shared__ int scan[2][kWave];
+    constexpr int RB = kWave * R;
+    constexpr int WSTEPS = kWinEntries / R;
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
+    const PairDesc pd = a.pairs[p];
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
+    if (lane < 33) alpha[lane] = a.alphabet[lane];
+
+    int score, i, j;
+    if (a.mode == SA_GLOBAL)
+    {
+        score = pd.num_strips > 0 ? a.pair_score[p] : -a.gap * (n + m);
+        i = m;
+        j = n;
+    }
+    else
+    {
+        uint64_t k = 0;
+        for (int s = lane; s < pd.num_strips; s += kWave) k = max(k, a.strip_best[pd.first_strip + s]);
+        for (int off = 32; off > 0; off >>= 1) k = max(k, shfl_xor_u64(k, off));
+        const int H = (int)(k >> (2 * kKeyRowBits));
+        if (H > 0)
+        {
+            score = H;
+            i = (int)(kKeyMask - ((k >> kKeyRowBits) & kKeyMask));
+            j = (int)(kKeyMask - (k & kKeyMask));
+        }
+        else
+        {
+            score = 0;  // no positive cell: maxIJ stays 0 (alignSequenceCPU.cpp:152)
+            i = 0;
+            j = 0;
+        }
+    }
+
+    int wb = -1, wlo = 0, whi = -1;
+    auto code_at = [&](int ci, int cj) -> int {
+        const int b = (ci - 1) / RB;
+        const int il = (ci - 1) - b * RB;
+        const int k = il / R, rho = il % R;
+        const int s = cj - 1 + k;
+        if (b != wb || s < wlo || s > whi)
+        {
+            __syncthreads();
+            wb = b;
+            whi = s;
+            wlo = max(0, s - WSTEPS + 1);
+            const StripDesc sd = a.strips[pd.first_strip + b];
+            const uint4 *src = a.masks + sd.mask_off + (uint64_t)wlo * R;
+            const int cnt = (whi - wlo + 1) * R;
+            for (int e = lane; e < cnt; e += kWave) win[e] = src[e];
+            __syncthreads();
+        }
+        const uint4 e = win[(s - wlo) * R + rho];
+        const uint32_t w0 = k < 32 ? e.x : e.y;
+        const uint32_t w1 = k < 32 ? e.z : e.w;
+        return (int)((w0 >> (k & 31)) & 1u) | (int)(((w1 >> (k & 31)) & 1u) << 1);
+    };
+
+    uint8_t *ops = a.ops + pd.out_off;
+    // text / pattern index of the first letter the walk emits (the start cell's)
+    const int ti0 = a.mode == SA_GLOBAL ? n - 1 : j - 1;
+    const int pi0 = a.mode == SA_GLOBAL ? m - 1 : i - 1;
+    int len = 0, ti, pi;
+    if (a.mode == SA_GLOBAL)
+    {
+        // traceBackNW (alignSequenceCPU.cpp:64-114): row 0 forces LEFT, column 0 forces TOP
+        ti = n - 1;
+        pi = m - 1;
+        while (i > 0 || j > 0)
+        {
+            const int d = j == 0 ? kTop : (i == 0 ? kLeft : code_at(i, j));
+            const int tt = d == kDiag || d == kLeft;
+            const int tp = d == kDiag || d == kTop;
+            if (lane == 0) ops[len] = (uint8_t)d;
+            ++len;
+            ti = max(0, ti - tt);
+            pi = max(0, pi - tp);
+            i -= tp;
+            j -= tt;
+        }
+    }
+    else
+    {
+        // traceBackSW (alignSequenceCPU.cpp:10-62): stop at STOP; a move into row 0 / column 0
+        // ends the walk before the index update.
+        ti = j - 1;
+        pi = i - 1;
+        while (i > 0 && j > 0)
+        {
+            const int d = code_at(i, j);
+            if (d == kStop) break;
+            const int tt = d == kDiag || d == kLeft;
+            const int tp = d == kDiag || d == kTop;
+            if (lane == 0) ops[len] = (uint8_t)d;
+            ++len;
+            i -= tp;
+            j -= tt;
+            if (i == 0 || j == 0) break;
+            ti = max(0, ti - tt);
+            pi = max(0, pi - tp);
+        }
+    }
+    if (lane == 0)
+    {
+        sa_result r;
+        r.score = score;
+        r.status = SA_OK;
+        r.num_alignment_bytes = (uint64_t)len;
+        r.start_text = (uint64_t)(int64_t)ti;
+        r.start_pattern = (uint64_t)(int64_t)pi;
+        a.results[p] = r;
+    }
+    __syncthreads();
+
+    // ops (walk order, i.e. reversed) -> letters (forward order). Letters only depend on how many
+    // text / pattern letters the later part of the path consumed, so each lane converts one chunk.
+    const int chunk = (len + kWave - 1) / kWave;
+    const int c0 = min(len, lane * chunk), c1 = min(len, c0 + chunk);
+    int nt = 0, np = 0;
+    for (int t = c0; t < c1; ++t)
+    {
+        const int d = ops[t];
+        nt += (d == kDiag || d == kLeft);
+        np += (d == kDiag || d == kTop);
+    }
+    scan[0][lane] = nt;
+    scan[1][lane] = np;
+    __syncthreads();
+    int bt = 0, bp = 0;
+    for (int l = 0; l < lane; ++l) { bt += scan[0][l]; bp += scan[1][l]; }
+    const char GAPC = alpha[a.A];
+    char *ot = a.out_text + pd.out_off;
+    char *op = a.out_pattern + pd.out_off;
+    int xt = ti0 - bt, xp = pi0 - bp;
+    for (int t = c0; t < c1; ++t)
+    {
+        const int d = ops[t];
+        const int tt = d == kDiag || d == kLeft;
+        const int tp = d == kDiag || d == kTop;
+        ot[len - 1 - t] = tt ? alpha[(int)a.text[pd.text_off + xt]] : GAPC;
+        op[len - 1 - t] = tp ? alpha[(int)a.pattern[pd.pattern_off + xp]] : GAPC;
+        xt -= tt;
+        xp -= tp;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// self test of the wave primitives the kernels rely on
+// ------------------------------------------------------------------------------------------------
+__global__ void selftest_kernel(int *out)
+{
+    const int lane = threadIdx.x;
+    const int v = 100 + lane;
+    out[0 * 64 + lane] = dpp_shr1(-1, v);   // expect lane-1 (lane 0: -1)
+    out[1 * 64 + lane] = dpp_shl1(-2, v);   // expect lane+1 (lane 63: -2)
+    out[2 * 64 + lane] = dpp_rol1(v);       // expect lane+1 mod 64
+    const uint64_t b = ballot((lane % 3) == 0);
+    uint32_t acc = 0;
+    writelane<5>(acc, (uint32_t)b);
+    writelane<6>(acc, (uint32_t)(b >> 32));
+    out[3 * 64 + lane] = (int)acc;
+    out[4 * 64 + lane] = __builtin_amdgcn_sbfe(0x18F70A05, 8 * (lane & 3), 8);  // 5, 10, -9, 24
+}
+
+}  // namespace sa
+
+// ==================================================================================================
+// host side
+// ==================================================================================================
+using namespace sa;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess) return fail(SA_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T>
+int dmalloc(T **p, size_t bytes)
+{
+    *p = nullptr;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc((void **)p, bytes) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return fail(SA_ERR_NOMEM, "device allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    return SA_OK;
+}
+
+}  // namespace
+
+struct sa_plan {
+    int device = 0;
+    int mode = 0, A = 0, gap = 0, R = 0, U = 0, key_bits = 12;
+    bool packed = false;
+    int num_cu = 0;
+    std::vector<PairDesc> pairs;
+    std::vector<StripDesc> strips;
+    char alphabet[33] = {0};
+    uint32_t epoch = 0;
+    hipStream_t own = nullptr;
+    // device
+    PairDesc *d_pairs = nullptr;
+    StripDesc *d_strips = nullptr;
+    int32_t *d_prof = nullptr, *d_table = nullptr;
+    int8_t *d_codes = nullptr;
+    uint32_t *d_masks = nullptr;
+    uint64_t *d_bnd = nullptr, *d_best = nullptr;
+    int32_t *d_score = nullptr;
+    Control *d_ctrl = nullptr;
+    uint8_t *d_ops = nullptr;
+    char *d_out_text = nullptr, *d_out_pattern = nullptr;
+    sa_result *d_results = nullptr;
+    const int8_t *d_text_in = nullptr, *d_pattern_in = nullptr;
+    uint64_t bytes_total = 0, bytes_masks = 0, out_bytes = 0;
+    bool filled = false;
+};
+
+namespace {
+
+int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
+{
+    int R = P->rows_per_lane;
+    if (const char *e = std::getenv("SA_ROWS_PER_LANE")) R = std::atoi(e);
+    if (R == 1 || R == 2 || R == 4 || R == 8 || R == 16 || R == 32) return R;
+    uint64_t mmax = 0;
+    for (int64_t p = 0; p < np; ++p) mmax = std::max<uint64_t>(mmax, pairs[p].pattern_len);
+    if (np >= 256)
+    {
+        // many independent pairs: one strip per pair where possible (no hand-offs at all)
+        int r = 1;
+        while (r < 32 && (uint64_t)kWave * r < mmax) r <<= 1;
+        return r;
+    }
+    // few long pairs: short strips keep the wavefront pipeline deep
+    return mmax > 16384 ? 2 : 1;
+}
+
+template <int R, bool LOCAL, bool PACKED>
+void launch_fill_t(const FillArgs &a, int grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((fill_kernel<R, LOCAL, PACKED>), dim3(grid), dim3(kWave), 0, st, a);
+}
+
+template <int R>
+void launch_fill_r(const FillArgs &a, bool local, bool packed, int grid, hipStream_t st)
+{
+    if (local)
+    {
+        if (packed) launch_fill_t<R, true, true>(a, grid, st);
+        else launch_fill_t<R, true, false>(a, grid, st);
+    }
+    else
+    {
+        if (packed) launch_fill_t<R, false, true>(a, grid, st);
+        else launch_fill_t<R, false, false>(a, grid, st);
+    }
+}
+
+void launch_fill(int R, const FillArgs &a, bool local, bool packed, int grid, hipStream_t st)
+{
+    switch (R)
+    {
+    case 1: launch_fill_r<1>(a, local, packed, grid, st); break;
+    case 2: launch_fill_r<2>(a, local, packed, grid, st); break;
+    case 4: launch_fill_r<4>(a, local, packed, grid, st); break;
+    case 8: launch_fill_r<8>(a, local, packed, grid, st); break;
+    case 16: launch_fill_r<16>(a, local, packed, grid, st); break;
+    default: launch_fill_r<32>(a, local, packed, grid, st); break;
+    }
+}
+
+void launch_tb(int R, const TbArgs &a, int np, hipStream_t st)
+{
+    switch (R)
+    {
+    case 1: hipLaunchKernelGGL(traceback_kernel<1>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(traceback_kernel<2>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 4: hipLaunchKernelGGL(traceback_kernel<4>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 8: hipLaunchKernelGGL(traceback_kernel<8>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 16: hipLaunchKernelGGL(traceback_kernel<16>, dim3(np), dim3(kWave), 0, st, a); break;
+    default: hipLaunchKernelGGL(traceback_kernel<32>, dim3(np), dim3(kWave), 0, st, a); break;
+    }
+}
+
+void free_plan(sa_plan *p)
+{
+    if (!p) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(p->device);
+    void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
+                    p->d_best, p->d_score, p->d_ctrl, p->d_ops, p->d_out_text, p->d_out_pattern, p->d_results};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (p->own) (void)hipStreamDestroy(p->own);
+    (void)hipSetDevice(cur);
+    delete p;
+}
+
+int bitlen(uint64_t v)
+{
+    int b = 0;
+    while (v) { ++b; v >>= 1; }
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *sa_last_error(void) { return g_err.c_str(); }
+int sa_abi_version(void) { return SA_ABI_VERSION; }
+
+int sa_device_count(int *count)
+{
+    HIP_TRY(hipGetDeviceCount(count));
+    return SA_OK;
+}
+
+int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, sa_plan **out)
+{
+    if (!P || !out || np < 0 || (np > 0 && !pairs) || !P->score_matrix)
+        return fail(SA_ERR_INVALID, "sa_plan_create: null argument");
+    *out = nullptr;
+    const int A = P->alphabet_size;
+    if (A < 1 || A > 32) return fail(SA_ERR_INVALID, "alphabet_size must be 1..32");
+    if (P->mode != SA_GLOBAL && P->mode != SA_LOCAL) return fail(SA_ERR_INVALID, "mode must be SA_GLOBAL or SA_LOCAL");
+    const int64_t g = P->gap_penalty;
+    int64_t smax = INT32_MIN, smin = INT32_MAX, sabs = 0;
+    for (int e = 0; e < A * A; ++e)
+    {
+        smax = std::max<int64_t>(smax, P->score_matrix[e]);
+        smin = std::min<int64_t>(smin, P->score_matrix[e]);
+        sabs = std::max<int64_t>(sabs, std::llabs((long long)P->score_matrix[e]));
+    }
+    // numeric limits of the engine: every intermediate fits in int32, local keys fit.
+    uint64_t hmax_local = 0;
+    for (int64_t p = 0; p < np; ++p)
+    {
+        const uint64_t n = pairs[p].text_len, m = pairs[p].pattern_len;
+        if (n >= (1u << kKeyRowBits) - 1 || m >= (1u << kKeyRowBits) - 1)
+            return fail(SA_ERR_UNSUPPORTED, "sequence longer than 2^21-2 letters");
+        const uint64_t span = n + m;
+        const uint64_t bound = ((uint64_t)sabs + (uint64_t)std::llabs(g)) * span + (uint64_t)std::llabs(g) * span;
+        if (bound >= (1ull << 30)) return fail(SA_ERR_UNSUPPORTED, "scores may exceed the int32 range");
+        const uint64_t h = g >= 0 ? (uint64_t)std::max<int64_t>(smax, 0) * std::min(n, m)
+                                  : ((uint64_t)sabs + (uint64_t)(-g)) * span;
+        hmax_local = std::max(hmax_local, h);
+    }
+    if (P->mode == SA_LOCAL && hmax_local >= (1ull << 22))
+        return fail(SA_ERR_UNSUPPORTED, "local scores may exceed 2^22");
+
+    sa_plan *pl = new sa_plan();
+    pl->device = device;
+    pl->mode = P->mode;
+    pl->A = A;
+    pl->gap = (int)g;
+    pl->R = choose_R(P, pairs, np);
+    pl->U = (16 / pl->R) > 4 ? 16 / pl->R : 4;
+    pl->key_bits = std::min(12, std::max(4, 30 - bitlen(hmax_local)));
+    const int64_t off2 = P->mode == SA_GLOBAL ? 2 * g : 0;
+    pl->packed = A <= 4;
+    for (int e = 0; e < A * A && pl->packed; ++e)
+    {
+        const int64_t v = P->score_matrix[e] + off2;
+        if (v < -128 || v > 127) pl->packed = false;
+    }
+    if (P->alphabet) std::memcpy(pl->alphabet, P->alphabet, std::min<size_t>(A + 1, 33));
+    else for (int c = 0; c <= A; ++c) pl->alphabet[c] = c == A ? '-' : (char)('A' + c);
+
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    auto restore = [&]() { (void)hipSetDevice(cur); };
+    if (hipSetDevice(device) != hipSuccess) { delete pl; restore(); return fail(SA_ERR_HIP, "hipSetDevice failed"); }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { delete pl; restore(); return fail(SA_ERR_HIP, "hipGetDeviceProperties failed"); }
+    pl->num_cu = prop.multiProcessorCount;
+
+    // ---- layout ----
+    const int R = pl->R, U = pl->U, RB = kWave * R;
+    uint64_t code_bytes = 0, mask_entries = 0, granules = 0, outb = 0;
+    pl->pairs.resize(np);
+    for (int64_t p = 0; p < np; ++p)
+    {
+        PairDesc &d = pl->pairs[p];
+        d.text_off = pairs[p].text_offset;
+        d.text_len = pairs[p].text_len;
+        d.pattern_off = pairs[p].pattern_offset;
+        d.pattern_len = pairs[p].pattern_len;
+        d.code_off = code_bytes;
+        code_bytes += kPad + d.text_len + 4 * kPad;
+        d.out_off = outb;
+        outb += d.text_len + d.pattern_len + 16;
+        d.first_strip = (int32_t)pl->strips.size();
+        const uint64_t n = d.text_len, m = d.pattern_len;
+        const int ns = (n == 0 || m == 0) ? 0 : (int)((m + RB - 1) / RB);
+        d.num_strips = ns;
+        const int nsteps = (int)(((n + kWave - 1) + U - 1) / U * U);
+        for (int b = 0; b < ns; ++b)
+        {
+            StripDesc s;
+            s.pair = (int32_t)p;
+            s.row0 = 1 + b * RB;
+            s.flags = (b > 0 ? kHasPrev : 0) | (b + 1 < ns ? kHasNext : 0);
+            s.nsteps = nsteps;
+            s.mask_off = mask_entries;
+            mask_entries += (uint64_t)nsteps * R;
+            s.bnd_in = b > 0 ? pl->strips.back().bnd_out : 0;
+            s.bnd_out = granules;
+            if (b + 1 < ns) granules += n + 8;
+            pl->strips.push_back(s);
+        }
+    }
+    if (pl->strips.size() >= (1u << 31)) { delete pl; restore(); return fail(SA_ERR_UNSUPPORTED, "too many strips"); }
+    pl->out_bytes = outb;
+    pl->bytes_masks = mask_entries * 16;
+
+    // ---- tables ----
+    std::vector<int32_t> prof(4, 0), table(A * A);
+    for (int e = 0; e < A * A; ++e) table[e] = (int32_t)(P->score_matrix[e] + off2);
+    if (pl->packed)
+        for (int cp = 0; cp < A; ++cp)
+        {
+            uint32_t w = 0;
+            for (int ct = 0; ct < A; ++ct) w |= (uint32_t)(table[cp * A + ct] & 0xff) << (8 * ct);
+            prof[cp] = (int32_t)w;
+        }
+
+    // ---- device buffers ----
+    int rc = SA_OK;
+    auto alloc = [&](auto **ptr, size_t bytes) {
+        if (rc == SA_OK) { rc = dmalloc(ptr, bytes); pl->bytes_total += bytes; }
+    };
+    alloc(&pl->d_pairs, sizeof(PairDesc) * std::max<size_t>(1, np));
+    alloc(&pl->d_strips, sizeof(StripDesc) * std::max<size_t>(1, pl->strips.size()));
+    alloc(&pl->d_prof, sizeof(int32_t) * 4);
+    alloc(&pl->d_table, sizeof(int32_t) * A * A);
+    alloc(&pl->d_codes, code_bytes + 16);
+    alloc(&pl->d_masks, pl->bytes_masks + 16);
+    alloc(&pl->d_bnd, granules * 8 + 16);
+    alloc(&pl->d_best, sizeof(uint64_t) * std::max<size_t>(1, pl->strips.size()));
+    alloc(&pl->d_score, sizeof(int32_t) * std::max<size_t>(1, np));
+    alloc(&pl->d_ctrl, sizeof(Control));
+    alloc(&pl->d_ops, outb + 16);
+    alloc(&pl->d_out_text, outb + 16);
+    alloc(&pl->d_out_pattern, outb + 16);
+    alloc(&pl->d_results, sizeof(sa_result) * std::max<size_t>(1, np));
+    if (rc != SA_OK) { free_plan(pl); restore(); return rc; }
+    if (hipStreamCreateWithFlags(&pl->own, hipStreamNonBlocking) != hipSuccess) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "stream creation failed"); }
+    bool okc = hipMemcpy(pl->d_pairs, pl->pairs.data(), sizeof(PairDesc) * np, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size(), hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(pl->d_prof, prof.data(), sizeof(int32_t) * 4, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemset(pl->d_codes, 0, code_bytes + 16) == hipSuccess &&
+               hipMemset(pl->d_bnd, 0, granules * 8 + 16) == hipSuccess &&
+               hipMemset(pl->d_best, 0, sizeof(uint64_t) * std::max<size_t>(1, pl->strips.size())) == hipSuccess;
+    if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
+    restore();
+    *out = pl;
+    return SA_OK;
+}
+
+int sa_plan_destroy(sa_plan *plan)
+{
+    free_plan(plan);
+    return SA_OK;
+}
+
+int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *stream)
+{
+    if (!pl || (!pl->pairs.empty() && (!d_text || !d_pattern))) return fail(SA_ERR_INVALID, "sa_plan_fill: null argument");
+    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(pl->device));
+    pl->d_text_in = (const int8_t *)d_text;
+    pl->d_pattern_in = (const int8_t *)d_pattern;
+    pl->epoch += 1;
+    if (pl->epoch == 0) pl->epoch = 1;
+    HIP_TRY(hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st));
+    const int np = (int)pl->pairs.size();
+    if (np > 0)
+    {
+        uint64_t nmax = 1;
+        for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, d.text_len);
+        const int gx = (int)std::min<uint64_t>((nmax + 255) / 256, 64);
+        for (int y0 = 0; y0 < np; y0 += 65535)
+        {
+            // pairs beyond 65535 are handled by re-basing the pair pointer
+            const int cnt = std::min(65535, np - y0);
+            hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
+                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->packed ? 8 : 1);
+        }
+        HIP_TRY(hipGetLastError());
+    }
+    const int ns = (int)pl->strips.size();
+    if (ns > 0)
+    {
+        FillArgs a;
+        a.pattern = (const int8_t *)d_pattern;
+        a.codes = pl->d_codes;
+        a.strips = pl->d_strips;
+        a.pairs = pl->d_pairs;
+        a.prof_tab = pl->d_prof;
+        a.score_tab = pl->d_table;
+        a.masks = pl->d_masks;
+        a.bnd = pl->d_bnd;
+        a.strip_best = pl->d_best;
+        a.pair_score = pl->d_score;
+        a.ctrl = pl->d_ctrl;
+        a.num_strips = ns;
+        a.gap = pl->gap;
+        a.A = pl->A;
+        a.epoch = pl->epoch;
+        a.key_bits = pl->key_bits;
+        const int grid = std::min(ns, std::max(1, pl->num_cu) * 8);
+        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->packed, grid, st);
+        HIP_TRY(hipGetLastError());
+    }
+    pl->filled = true;
+    HIP_TRY(hipSetDevice(cur));
+    return SA_OK;
+}
+
+int sa_plan_traceback(sa_plan *pl, void *stream)
+{
+    if (!pl || !pl->filled) return fail(SA_ERR_INVALID, "sa_plan_traceback: plan not filled");
+    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    const int np = (int)pl->pairs.size();
+    if (np == 0) return SA_OK;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(pl->device));
+    TbArgs a;
+    a.text = pl->d_text_in;
+    a.pattern = pl->d_pattern_in;
+    a.strips = pl->d_strips;
+    a.pairs = pl->d_pairs;
+    a.masks = (const uint4 *)pl->d_masks;
+    a.strip_best = pl->d_best;
+    a.pair_score = pl->d_score;
+    a.ops = pl->d_ops;
+    a.out_text = pl->d_out_text;
+    a.out_pattern = pl->d_out_pattern;
+    a.results = pl->d_results;
+    a.mode = pl->mode;
+    a.gap = pl->gap;
+    a.A = pl->A;
+    std::memcpy(a.alphabet, pl->alphabet, 33);
+    launch_tb(pl->R, a, np, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipSetDevice(cur));
+    return SA_OK;
+}
+
+int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
+{
+    if (!pl || !out) return fail(SA_ERR_INVALID, "sa_plan_fetch_results: null argument");
+    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(pl->device));
+    Control ctrl;
+    HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
+    if (!pl->pairs.empty())
+        HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipSetDevice(cur));
+    if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
+    return SA_OK;
+}
+
+int sa_plan_fetch_alignment(sa_plan *pl, int64_t index, char *at, char *ap, uint64_t cap, void *stream)
+{
+    if (!pl || index < 0 || index >= (int64_t)pl->pairs.size()) return fail(SA_ERR_INVALID, "sa_plan_fetch_alignment: bad index");
+    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(pl->device));
+    sa_result r;
+    HIP_TRY(hipMemcpyAsync(&r, pl->d_results + index, sizeof(r), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (r.num_alignment_bytes > cap) { (void)hipSetDevice(cur); return fail(SA_ERR_INVALID, "output capacity too small"); }
+    const uint64_t off = pl->pairs[index].out_off;
+    if (r.num_alignment_bytes)
+    {
+        if (at) HIP_TRY(hipMemcpyAsync(at, pl->d_out_text + off, r.num_alignment_bytes, hipMemcpyDeviceToHost, st));
+        if (ap) HIP_TRY(hipMemcpyAsync(ap, pl->d_out_pattern + off, r.num_alignment_bytes, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    HIP_TRY(hipSetDevice(cur));
+    return SA_OK;
+}
+
+int sa_plan_info(const sa_plan *pl, int64_t *num_strips, int32_t *rows_per_lane, uint64_t *device_bytes,
+                 uint64_t *mask_bytes)
+{
+    if (!pl) return fail(SA_ERR_INVALID, "sa_plan_info: null plan");
+    if (num_strips) *num_strips = (int64_t)pl->strips.size();
+    if (rows_per_lane) *rows_per_lane = pl->R;
+    if (device_bytes) *device_bytes = pl->bytes_total;
+    if (mask_bytes) *mask_bytes = pl->bytes_masks;
+    return SA_OK;
+}
+
+const void *sa_plan_device_results(const sa_plan *pl) { return pl ? (const void *)pl->d_results : nullptr; }
+
+int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *pattern, uint64_t m, int device,
+                  sa_result *out, char *at, char *ap, uint64_t cap, double *fill_us)
+{
+    if (!P || !out || (n && !text) || (m && !pattern)) return fail(SA_ERR_INVALID, "sa_align_pair: null argument");
+    const bool fillOnly = !at && !ap;  // -DBENCHMARK contract: DP fill only
+    if (!fillOnly && cap < n + m) return fail(SA_ERR_INVALID, "sa_align_pair: output capacity below text_len + pattern_len");
+    for (uint64_t x = 0; x < n; ++x)
+        if (text[x] < 0 || text[x] >= P->alphabet_size) return fail(SA_ERR_INVALID, "text byte outside the alphabet");
+    for (uint64_t x = 0; x < m; ++x)
+        if (pattern[x] < 0 || pattern[x] >= P->alphabet_size) return fail(SA_ERR_INVALID, "pattern byte outside the alphabet");
+    sa_pair pr{0, n, 0, m};
+    sa_plan *pl = nullptr;
+    int rc = sa_plan_create(P, &pr, 1, device, &pl);
+    if (rc) return rc;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    int8_t *dt = nullptr, *dp = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto cleanup = [&]() {
+        if (dt) (void)hipFree(dt);
+        if (dp) (void)hipFree(dp);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        sa_plan_destroy(pl);
+        (void)hipSetDevice(cur);
+    };
+    if ((rc = dmalloc(&dt, n + 16)) || (rc = dmalloc(&dp, m + 16))) { cleanup(); return rc; }
+    if (hipMemcpyAsync(dt, text, n, hipMemcpyHostToDevice, pl->own) != hipSuccess ||
+        hipMemcpyAsync(dp, pattern, m, hipMemcpyHostToDevice, pl->own) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    {
+        cleanup();
+        return fail(SA_ERR_HIP, "sa_align_pair: upload failed");
+    }
+    (void)hipEventRecord(e0, pl->own);
+    rc = sa_plan_fill(pl, dt, dp, pl->own);
+    (void)hipEventRecord(e1, pl->own);
+    if (!rc && !fillOnly) rc = sa_plan_traceback(pl, pl->own);
+    if (!rc && !fillOnly) rc = sa_plan_fetch_results(pl, out, pl->own);
+    if (!rc && !fillOnly) rc = sa_plan_fetch_alignment(pl, 0, at, ap, cap, pl->own);
+    if (!rc && fillOnly && hipStreamSynchronize(pl->own) != hipSuccess) rc = fail(SA_ERR_HIP, "sa_align_pair: sync failed");
+    if (!rc && fill_us)
+    {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        *fill_us = 1000.0 * ms;
+    }
+    cleanup();
+    return rc;
+}
+
+int sa_selftest(int device)
+{
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(device));
+    int *d = nullptr;
+    HIP_TRY(hipMalloc(&d, 5 * 64 * sizeof(int)));
+    hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 0, 0, d);
+    std::vector<int> h(5 * 64);
+    HIP_TRY(hipMemcpy(h.data(), d, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_TRY(hipFree(d));
+    HIP_TRY(hipSetDevice(cur));
+    uint64_t b = 0;
+    for (int l = 0; l < 64; ++l)
+        if (l % 3 == 0) b |= 1ull << l;
+    const int sbfe[4] = {5, 10, -9, 24};
+    for (int l = 0; l < 64; ++l)
+    {
+        if (h[l] != (l == 0 ? -1 : 100 + l - 1)) return fail(SA_ERR_UNSUPPORTED, "DPP wave_shr:1 mismatch at lane " + std::to_string(l));
+        if (h[64 + l] != (l == 63 ? -2 : 100 + l + 1)) return fail(SA_ERR_UNSUPPORTED, "DPP wave_shl:1 mismatch at lane " + std::to_string(l));
+        if (h[128 + l] != 100 + (l + 1) % 64) return fail(SA_ERR_UNSUPPORTED, "DPP wave_rol:1 mismatch at lane " + std::to_string(l));
+        const int wl = l == 5 ? (int)(uint32_t)b : (l == 6 ? (int)(uint32_t)(b >> 32) : 0);
+        if (h[192 + l] != wl) return fail(SA_ERR_UNSUPPORTED, "ballot/writelane mismatch at lane " + std::to_string(l));
+        if (h[256 + l] != sbfe[l & 3]) return fail(SA_ERR_UNSUPPORTED, "v_bfe_i32 mismatch at lane " + std::to_string(l));
+    }
+    return SA_OK;
+}
+
+}  // extern "C"

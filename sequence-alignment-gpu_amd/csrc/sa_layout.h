@@ -1,0 +1,56 @@
+// Internal data layout shared by the fill and traceback kernels and the host planner.
+//
+// A pair's DP matrix (pattern rows 1..m, text columns 1..n; row 0 / column 0 are the boundary)
+// is cut into horizontal STRIPS of 64*R rows. One wave64 owns a strip: lane k owns the R
+// consecutive rows  row0 + k*R + rho  (rho = 0..R-1) and sweeps the text left to right, lane k
+// working on column  j = s - k + 1  at step s (a one-column skew per lane, the anti-diagonal
+// wavefront). A strip therefore takes n + 63 steps.
+//
+// DIRECTIONS. At every (step s, row-slot rho) the wave produces, for its 64 cells, two 64-bit
+// planes from wave ballots: bit k of plane0/plane1 is bit 0/1 of the reference DIRECTION code
+// (LEFT=0, DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) of lane k's cell. They are stored
+// as one 16-byte entry {plane0, plane1}; entry (s, rho) of strip b lives at
+//     masks[strip.mask_off + s*R + rho].
+// That is 2 bits per cell written to HBM (the reference writes 1 byte per cell,
+// alignSequenceGPU.cu:142); the algorithmic figure used for the roofline stays 1 B/cell.
+//
+// STRIP HAND-OFF. A strip's bottom row feeds the next strip's first row. It travels through a
+// granule array in global memory: granule c-1 holds {tag = epoch, value} of column c as one
+// 8-byte write-through store, so the consumer needs no flag and no fence (a tag match means the
+// value is there); the per-call epoch makes stale granules from earlier calls unreadable.
+#pragma once
+#include <stdint.h>
+
+namespace sa {
+
+constexpr int kWave = 64;
+constexpr int kPad = 64;          // text-code padding before/after each pair
+constexpr int kKeyRowBits = 21;   // local-alignment best-cell key: H:22 | ~row:21 | ~col:21
+constexpr uint64_t kKeyMask = (1ull << kKeyRowBits) - 1;
+
+struct StripDesc {
+    int32_t pair;       // owning pair
+    int32_t row0;       // first DP row (1-based) of the strip
+    int32_t flags;      // kHasPrev | kHasNext
+    int32_t nsteps;     // steps this strip runs (n + 63 rounded up to the body length)
+    uint64_t mask_off;  // first 16-byte direction entry
+    uint64_t bnd_in;    // granule index of the predecessor's bottom row (kHasPrev)
+    uint64_t bnd_out;   // granule index of this strip's bottom row (kHasNext)
+};
+enum : int32_t { kHasPrev = 1, kHasNext = 2 };
+
+struct PairDesc {
+    uint64_t text_off, text_len, pattern_off, pattern_len;
+    uint64_t code_off;     // start of this pair's padded text-code block
+    uint64_t out_off;      // start of this pair's output region (capacity text_len+pattern_len)
+    int32_t first_strip, num_strips;
+};
+
+// Per-launch control block (zeroed by the host before every fill).
+struct Control {
+    uint32_t queue_head;   // dynamic strip queue
+    uint32_t abort_flag;   // set when a hand-off times out
+    uint32_t pad[2];
+};
+
+}  // namespace sa

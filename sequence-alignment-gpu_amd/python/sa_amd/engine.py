@@ -1,0 +1,159 @@
+"""ctypes binding of the C ABI in include/sa_hip.h (libsa_hip.so).
+
+The product path: every call goes to the HIP engine. If the shared library is missing this
+module raises at import time — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), "..", ".."))
+LIB_PATH = os.environ.get("SA_HIP_LIB", os.path.join(PKG_ROOT, "lib", "libsa_hip.so"))
+
+SA_GLOBAL, SA_LOCAL = 0, 1
+STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4: "SA_ERR_UNSUPPORTED",
+          5: "SA_ERR_TIMEOUT"}
+
+# Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
+EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
+           "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
+           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest")
+
+
+class SaParams(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int32), ("alphabet_size", ctypes.c_int32), ("gap_penalty", ctypes.c_int32),
+                ("rows_per_lane", ctypes.c_int32), ("score_matrix", ctypes.c_void_p), ("alphabet", ctypes.c_char_p)]
+
+
+class SaPair(ctypes.Structure):
+    _fields_ = [("text_offset", ctypes.c_uint64), ("text_len", ctypes.c_uint64),
+                ("pattern_offset", ctypes.c_uint64), ("pattern_len", ctypes.c_uint64)]
+
+
+class SaResult(ctypes.Structure):
+    _fields_ = [("score", ctypes.c_int32), ("status", ctypes.c_int32), ("num_alignment_bytes", ctypes.c_uint64),
+                ("start_text", ctypes.c_uint64), ("start_pattern", ctypes.c_uint64)]
+
+
+class SaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"HIP engine not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
+    L.sa_align_pair.argtypes = [ctypes.POINTER(SaParams), P, U64, P, U64, I, ctypes.POINTER(SaResult), P, P, U64,
+                                ctypes.POINTER(ctypes.c_double)]
+    L.sa_plan_create.argtypes = [ctypes.POINTER(SaParams), ctypes.POINTER(SaPair), ctypes.c_int64, I,
+                                 ctypes.POINTER(P)]
+    L.sa_plan_destroy.argtypes = [P]
+    L.sa_plan_fill.argtypes = [P, P, P, P]
+    L.sa_plan_traceback.argtypes = [P, P]
+    L.sa_plan_fetch_results.argtypes = [P, ctypes.POINTER(SaResult), P]
+    L.sa_plan_fetch_alignment.argtypes = [P, ctypes.c_int64, P, P, U64, P]
+    L.sa_plan_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    L.sa_plan_device_results.argtypes = [P]
+    L.sa_plan_device_results.restype = P
+    L.sa_device_count.argtypes = [ctypes.POINTER(I)]
+    L.sa_last_error.restype = ctypes.c_char_p
+    L.sa_selftest.argtypes = [I]
+    for name in EXPORTS:
+        getattr(L, name)
+    return L
+
+
+lib = _load()
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise SaError(rc, lib.sa_last_error().decode(errors="replace"))
+
+
+def _params(mode: int, S: np.ndarray, gap: int, alphabet: bytes | None, rows_per_lane: int):
+    S = np.ascontiguousarray(S, dtype=np.int32).ravel()
+    A = int(round(np.sqrt(S.size)))
+    if A * A != S.size:
+        raise ValueError("score matrix must be square")
+    if alphabet is None:
+        alphabet = b"ATCG-" if A == 4 else b"ARNDCQEGHILKMFPSTWYVBZX-"[: A] + b"-"
+    p = SaParams(mode, A, gap, rows_per_lane, S.ctypes.data, alphabet)
+    return p, S, alphabet
+
+
+def selftest(device: int = 0) -> None:
+    _check(lib.sa_selftest(device))
+
+
+def align_pair(mode: int, text: np.ndarray, pattern: np.ndarray, S: np.ndarray, gap: int,
+               alphabet: bytes | None = None, device: int = 0, rows_per_lane: int = 0) -> dict:
+    """One pair from host memory through the HIP engine (synchronous)."""
+    text = np.ascontiguousarray(text, dtype=np.int8)
+    pattern = np.ascontiguousarray(pattern, dtype=np.int8)
+    p, S_keep, alpha_keep = _params(mode, S, gap, alphabet, rows_per_lane)
+    n, m = len(text), len(pattern)
+    cap = max(1, n + m)
+    at = ctypes.create_string_buffer(cap)
+    ap = ctypes.create_string_buffer(cap)
+    res = SaResult()
+    fill_us = ctypes.c_double()
+    _check(lib.sa_align_pair(ctypes.byref(p), text.ctypes.data, n, pattern.ctypes.data, m, device,
+                             ctypes.byref(res), at, ap, cap, ctypes.byref(fill_us)))
+    L = res.num_alignment_bytes
+    return {"score": res.score, "num_bytes": L, "start_text": res.start_text, "start_pattern": res.start_pattern,
+            "aligned_text": at.raw[:L].decode(), "aligned_pattern": ap.raw[:L].decode(), "fill_us": fill_us.value}
+
+
+class Plan:
+    """Many pairs, device-resident arenas, explicit stream (for benches and the batch path)."""
+
+    def __init__(self, mode: int, S: np.ndarray, gap: int, pairs: list[tuple[int, int, int, int]],
+                 device: int = 0, alphabet: bytes | None = None, rows_per_lane: int = 0):
+        self._p, self._S, self._alpha = _params(mode, S, gap, alphabet, rows_per_lane)
+        arr = (SaPair * max(1, len(pairs)))(*[SaPair(*pr) for pr in pairs])
+        self.num_pairs = len(pairs)
+        self.pairs = pairs
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(lib.sa_plan_create(ctypes.byref(self._p), arr, len(pairs), device, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            lib.sa_plan_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+    def info(self) -> dict:
+        ns, r, db, mb = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_uint64()
+        _check(lib.sa_plan_info(self.handle, ctypes.byref(ns), ctypes.byref(r), ctypes.byref(db), ctypes.byref(mb)))
+        return {"num_strips": ns.value, "rows_per_lane": r.value, "device_bytes": db.value, "mask_bytes": mb.value}
+
+    def fill(self, d_text: int, d_pattern: int, stream: int | None = None) -> None:
+        _check(lib.sa_plan_fill(self.handle, d_text, d_pattern, stream))
+
+    def traceback(self, stream: int | None = None) -> None:
+        _check(lib.sa_plan_traceback(self.handle, stream))
+
+    def results(self, stream: int | None = None) -> list[dict]:
+        out = (SaResult * max(1, self.num_pairs))()
+        _check(lib.sa_plan_fetch_results(self.handle, out, stream))
+        return [{"score": r.score, "num_bytes": r.num_alignment_bytes, "start_text": r.start_text,
+                 "start_pattern": r.start_pattern} for r in out[: self.num_pairs]]
+
+    def alignment(self, index: int, stream: int | None = None) -> tuple[str, str]:
+        cap = max(1, self.pairs[index][1] + self.pairs[index][3])
+        at = ctypes.create_string_buffer(cap)
+        ap = ctypes.create_string_buffer(cap)
+        _check(lib.sa_plan_fetch_alignment(self.handle, index, at, ap, cap, stream))
+        r = self.results(stream)[index]
+        return at.raw[: r["num_bytes"]].decode(), ap.raw[: r["num_bytes"]].decode()

@@ -1,0 +1,174 @@
+"""GPU parity: the HIP engine (through the C ABI, include/sa_hip.h) against the reference's own outputs
+(tests/golden/*, produced by alignSequenceCPU of the reference) and against the oracle on seeded inputs.
+Bit-exact: score, aligned text, aligned pattern, start indices."""
+from __future__ import annotations
+
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import encode, matrix, same_result
+from sa_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from sa_amd import engine
+    engine.selftest(0)
+    return engine
+
+
+def _inputs(case):
+    A = case["A"]
+    return encode(case["text"], A), encode(case["pattern"], A), matrix(case["matrix"], A)
+
+
+def test_wave_primitives_selftest(eng):
+    eng.selftest(0)
+
+
+def test_known_answers(eng, golden):
+    for case in golden["known_answers.json"]:
+        t, p, S = _inputs(case)
+        got = eng.align_pair(case["mode"], t, p, S, case["gap"])
+        assert same_result(got, case["result"]), case["name"]
+        if case["expect_score"] is not None:
+            assert got["score"] == case["expect_score"]
+
+
+def test_data_pairs_one_shot(eng, golden):
+    d = golden["data_pairs.json"]
+    seqs = d["sequences"]
+    for case in d["cases"]:
+        A = case["A"]
+        got = eng.align_pair(case["mode"], encode(seqs[case["text"]], A), encode(seqs[case["pattern"]], A),
+                             matrix(case["matrix"], A), case["gap"])
+        assert same_result(got, case["result"]), (case["text"], case["pattern"], case["mode"])
+
+
+def test_data_pairs_batched(eng, golden):
+    """tests.cu:463-551 as ONE plan per (mode, alphabet): many pairs per fill launch."""
+    from sa_amd.batch import DeviceBatch
+    d = golden["data_pairs.json"]
+    seqs = d["sequences"]
+    key = lambda c: (c["mode"], c["A"], c["gap"], c["matrix"])
+    cases = sorted(d["cases"], key=key)
+    for (mode, A, gap, mat), grp in itertools.groupby(cases, key=key):
+        grp = list(grp)
+        b = DeviceBatch(mode, matrix(mat, A), gap, [encode(seqs[c["text"]], A) for c in grp],
+                        [encode(seqs[c["pattern"]], A) for c in grp])
+        res = b.run()
+        for k, c in enumerate(grp):
+            at, ap = b.alignment(k)
+            got = dict(res[k], aligned_text=at, aligned_pattern=ap)
+            assert same_result(got, c["result"]), (c["text"], c["pattern"], mode)
+        b.close()
+
+
+@pytest.mark.parametrize("rows_per_lane", [0, 1, 2, 4, 8, 16, 32])
+def test_random_pairs(eng, golden, rows_per_lane):
+    """Edge lengths (1..1000 around multiples of 64), ties, zero-score local alignments, asymmetric and
+    wide-range matrices, pattern longer than text; every strip height of the engine."""
+    for k, case in enumerate(golden["random_pairs.json"]):
+        t, p, S = _inputs(case)
+        got = eng.align_pair(case["mode"], t, p, S, case["gap"], rows_per_lane=rows_per_lane)
+        assert same_result(got, case["result"]), (k, case["tag"], len(t), len(p))
+
+
+@pytest.mark.parametrize("rows_per_lane", [1, 2, 4, 32])
+def test_seeded_vs_oracle(eng, rows_per_lane):
+    """Multi-strip hand-offs (pattern >> 64*R rows) on seeded DNA and protein pairs."""
+    rng = np.random.default_rng(1000 + rows_per_lane)
+    blast = synthetic.blast_matrix()
+    for k in range(12):
+        A = 4 if k % 3 else 23
+        S = blast if A == 4 else matrix("blosum62", 23)
+        n = int(rng.integers(500, 3000))
+        m = int(rng.integers(64, n + 1))
+        t = synthetic.random_sequence(int(rng.integers(1 << 30)), n, A)
+        p = synthetic.mutate(t, k, A, m) if k % 2 else synthetic.random_sequence(k + 99, m, A)
+        mode = k % 2
+        gap = int(rng.choice([1, 5, 11]))
+        exp = oracle.align(mode, t, p, S, gap)
+        got = eng.align_pair(mode, t, p, S, gap, rows_per_lane=rows_per_lane)
+        got.pop("fill_us")
+        assert got == exp, (k, n, m, mode)
+
+
+def _large_inputs(case):
+    A = case["letters"]
+    t = synthetic.random_sequence(case["text_seed"], case["n"], A)
+    p = (synthetic.random_sequence(case["pattern_seed"], case["m"], A) if case["pattern_kind"] == "rand"
+         else synthetic.mutate(t, case["pattern_seed"], A, case["m"]))
+    S = matrix(case["matrix"], 4 if case["matrix"] == "blast" else 23)
+    return t, p, S
+
+
+def test_large_configs(eng, golden):
+    """BASELINE.json configs 2-5 at their full sizes vs the reference's recorded outputs."""
+    for case in golden["large.json"]:
+        t, p, S = _large_inputs(case)
+        got = eng.align_pair(case["mode"], t, p, S, case["gap"])
+        assert same_result(got, case["result"]), case["name"]
+
+
+def _score_of(at: str, ap: str, S: np.ndarray, gap: int, A: int) -> int:
+    alpha = "ATCG" if A == 4 else "ARNDCQEGHILKMFPSTWYVBZX"
+    lut = {c: i for i, c in enumerate(alpha)}
+    s = 0
+    for x, y in zip(at, ap):
+        if x == "-" or y == "-":
+            s -= gap
+        else:
+            s += int(S[lut[y], lut[x]])  # S[pattern][text]
+    return s
+
+
+def test_full_size_properties(eng):
+    """Size-independent checks at the headline size: the alignment re-scores to the reported score,
+    ungapped strings are the inputs (global) or substrings at the reported starts (local)."""
+    S = synthetic.blast_matrix()
+    n = m = 32768
+    t = synthetic.random_sequence(21, n, 4)
+    p = synthetic.mutate(t, 22, 4, m)
+    alpha = np.array(list("ATCG"))
+    for mode in (0, 1):
+        got = eng.align_pair(mode, t, p, S, 5)
+        at, ap = got["aligned_text"], got["aligned_pattern"]
+        assert _score_of(at, ap, S, 5, 4) == got["score"]
+        tu, pu = at.replace("-", ""), ap.replace("-", "")
+        if mode == 0:
+            assert tu == "".join(alpha[t]) and pu == "".join(alpha[p])
+        else:
+            # local starts are "first aligned index" or one less (reference quirk, traceBackSW :45-53)
+            full_t, full_p = "".join(alpha[t]), "".join(alpha[p])
+            assert tu in full_t and pu in full_p
+            assert full_t.find(tu, max(0, got["start_text"] - 1)) in (got["start_text"], got["start_text"] + 1)
+
+
+def test_batch_plan_config5(eng, golden):
+    """Config 5 shape: many 2048^2 pairs in one plan; the recorded pairs match the reference."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    N = 256
+    texts = [synthetic.random_sequence(1000 + 2 * i, 2048, 4) for i in range(N)]
+    pats = [synthetic.random_sequence(1001 + 2 * i, 2048, 4) for i in range(N)]
+    b = DeviceBatch(0, S, 5, texts, pats)
+    res = b.run()
+    recorded = {c["name"]: c for c in golden["large.json"] if c["name"].startswith("cfg5_batch_pair_")}
+    for i in range(8):
+        at, ap = b.alignment(i)
+        assert same_result(dict(res[i], aligned_text=at, aligned_pattern=ap), recorded[f"cfg5_batch_pair_{i}"]["result"])
+    for i in (17, 101, 255):  # a few more against the oracle
+        at, ap = b.alignment(i)
+        exp = oracle.align(0, texts[i], pats[i], S, 5)
+        assert dict(res[i], aligned_text=at, aligned_pattern=ap) == exp
+    # repeated fills reuse the plan (epoch-tagged hand-offs) and give identical results
+    res2 = b.run()
+    assert res2 == res
+    b.close()
