@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X alignment engine — BASELINE.json metric:
+"GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA NW, 1/2/4/8 GPU".
+
+Default workload (--workload headline): one step = the DP fill of a 32768 x 32768 DNA global
+(Needleman-Wunsch) alignment, blast scores (+5/-4), gap 5, i.i.d. uniform synthetic sequences
+(splitmix64 seeds 6/7), inputs resident in HBM, direction matrix written to HBM — the reference's
+throughput convention (tests/benchmarks.cu:102-187: fill + direction matrix, no traceback; our
+traceback is timed separately and reported as e2e). With --gpus N every rank aligns its own pair
+(a single pair does not shard: replicas, weak scaling); value = all ranks' cells / max-over-ranks time.
+
+--workload batch: BASELINE.json config 5 — 4096 independent 2048 x 2048 DNA global pairs sharded
+pair i -> rank i mod N, one fill + traceback per step per rank, scores gathered to rank 0 over
+RCCL (torch.distributed 'nccl'); strong scaling.
+
+Prints ONE JSON line on rank 0. Launch N>1 with torch.distributed.run (see README/DESIGN).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["headline", "local", "batch"], default="headline")
+    ap.add_argument("--size", type=int, default=32768)
+    ap.add_argument("--rows-per-lane", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
+    return ap.parse_args()
+
+
+def cpu_baseline(mode: str, n: int, rows: int, seeds=(6, 7)) -> dict:
+    """Single-core CPU fill on a bounded sample of the same workload, on this host. Prefers the
+    reference's own CPU code (oracle/_ref/ref_align, built from /root/reference), else the oracle port."""
+    ref = os.path.join(ROOT, "oracle", "_ref", "ref_align")
+    cells = rows * n
+    if os.path.exists(ref):
+        with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+            f.write("5 -4 -4 -4\n-4 5 -4 -4\n-4 -4 5 -4\n-4 -4 -4 5\n")
+            mat = f.name
+        try:
+            out = subprocess.run([ref, "fillbench", mode, str(rows + 1), str(n + 1), str(seeds[0]), str(seeds[1]),
+                                  "4", "5", mat, "1"], capture_output=True, text=True, check=True, timeout=600)
+            us = json.loads(out.stdout.strip().splitlines()[-1])["us"]
+        finally:
+            os.unlink(mat)
+        kind = "reference"
+    else:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        from sa_amd import synthetic
+        t = synthetic.random_sequence(seeds[0], n, 4)
+        p = synthetic.random_sequence(seeds[1], rows, 4)
+        M = np.empty((rows + 1) * (n + 1), np.uint8)
+        t0 = time.perf_counter()
+        oracle.fill_only(0 if mode == "global" else 1, t, p, synthetic.blast_matrix(), 5, M)
+        us = (time.perf_counter() - t0) * 1e6
+        kind = "port"
+    return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 1, "kind": kind,
+            "sample": f"{mode} fill {rows}x{n} DNA blast gap 5 (same synthetic stream), 1 thread, "
+                      f"{us / 1e6:.2f} s"}
+
+
+def load_traffic(workload: str):
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(p):
+        d = json.load(open(p))
+        return d.get(workload)
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    from sa_amd import engine, synthetic
+    from sa_amd.batch import DeviceBatch
+
+    S = synthetic.blast_matrix()
+    gap = 5
+    if args.workload in ("headline", "local"):
+        n = m = args.size
+        mode = 0 if args.workload == "headline" else 1
+        t = synthetic.random_sequence(6 + 1000 * rank, n, 4)
+        p = synthetic.random_sequence(7 + 1000 * rank, m, 4)
+        job = DeviceBatch(mode, S, gap, [t], [p], device=local, rows_per_lane=args.rows_per_lane)
+        cells_rank = n * m
+        pairs_rank = 1
+        workload = {"workload": ("dna_global" if mode == 0 else "dna_local") + f"_{n}x{m}", "pairs_per_gpu": 1,
+                    "text_len": n, "pattern_len": m, "score": "blast +5/-4", "gap": gap,
+                    "parallelism": f"replicas{world}"}
+    else:
+        npairs, L = 4096, 2048
+        mine = list(range(rank, npairs, world))
+        texts = [synthetic.random_sequence(1000 + 2 * i, L, 4) for i in mine]
+        pats = [synthetic.random_sequence(1001 + 2 * i, L, 4) for i in mine]
+        job = DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)
+        cells_rank = len(mine) * L * L
+        pairs_rank = len(mine)
+        workload = {"workload": f"dna_global_batch_{npairs}x{L}x{L}", "pairs_total": npairs, "text_len": L,
+                    "pattern_len": L, "score": "blast +5/-4", "gap": gap, "parallelism": f"pairs_sharded{world}"}
+    info = job.plan.info()
+    stream = torch.cuda.current_stream(local)
+
+    def step():
+        job.fill()
+        if args.workload == "batch":
+            job.traceback()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(local)
+    # per-launch fill timing with HIP events on the stream the engine launches on (torch's current stream)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(local)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        evs[k][0].record(stream)
+        step()
+        evs[k][1].record(stream)
+    torch.cuda.synchronize(local)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = [a.elapsed_time(b) for a, b in evs]
+    res = job.results()  # checks the abort flag of the last fill
+
+    # traceback / end-to-end, outside the timed region (headline: reported only)
+    torch.cuda.synchronize(local)
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(stream)
+    job.fill()
+    e1.record(stream)
+    job.traceback()
+    e2.record(stream)
+    res = job.results()
+    fill_ms_e2e, tb_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
+
+    tmax = elapsed
+    scores = [r["score"] for r in res]
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        tmax = float(tt.item())
+        if args.workload == "batch":
+            # the batch path's exchange step: per-rank score shards gathered to rank 0 over RCCL
+            mine_t = torch.tensor(scores, dtype=torch.int32, device="cuda")
+            width = (4096 + world - 1) // world
+            pad = torch.full((width,), -2**31, dtype=torch.int32, device="cuda")
+            pad[: len(scores)] = mine_t
+            gathered = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
+            dist.gather(pad, gathered, dst=0)
+    cells_total = cells_rank * world
+    value = cells_total * args.steps / tmax / 1e9
+    if rank == 0:
+        avg_ms = float(np.mean(launch_ms))
+        bytes_per_launch = float(cells_rank)  # algorithmic: 1 DIRECTION byte per cell
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        traffic = load_traffic(workload["workload"])
+        out = {
+            "metric": "GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA NW",
+            "value": round(value, 3),
+            "unit": "GCUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.workload != "batch" else "strong",
+            "vs_baseline": None,
+            "dtype": "int32",
+            "data": "synthetic (splitmix64 i.i.d. DNA, blast +5/-4, gap 5)",
+            "config": dict(workload, rows_per_lane=info["rows_per_lane"], strips_per_gpu=info["num_strips"]),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic},
+            "fill_ms_per_launch": {"mean": round(avg_ms, 4), "min": round(min(launch_ms), 4),
+                                   "median": round(float(np.median(launch_ms)), 4)},
+            "gcups_best_launch": round(cells_rank / (min(launch_ms) * 1e-3) / 1e9 * world, 3),
+            "gcups_reference_convention": round(pairs_rank * (workload["text_len"] + 1) * (workload["pattern_len"] + 1)
+                                                / (min(launch_ms) * 1e-3) / 1e9 * world, 3),
+            "e2e_ms": {"fill": round(fill_ms_e2e, 4), "traceback": round(tb_ms, 4)},
+            "direction_bytes_physical_per_launch": info["mask_bytes"],
+            "sample_result": {"pair0_score": scores[0] if scores else None, "pairs_per_gpu": pairs_rank},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            if args.workload == "batch":
+                out["cpu_baseline"] = cpu_baseline("global", 2048, args.cpu_rows or 2048 * 16, seeds=(1000, 1001))
+            else:
+                out["cpu_baseline"] = cpu_baseline("global" if args.workload == "headline" else "local",
+                                                   args.size, args.cpu_rows or args.size)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

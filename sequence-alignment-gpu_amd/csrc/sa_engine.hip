@@ -56,19 +56,32 @@ __device__ __forceinline__ int dpp_shr1(int old, int src) { return __builtin_amd
 __device__ __forceinline__ int dpp_shl1(int old, int src) { return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false); }
 __device__ __forceinline__ int dpp_rol1(int src) { return __builtin_amdgcn_update_dpp(src, src, 0x134, 0xf, 0xf, false); }
 
+// v_writelane_b32 through the LLVM intrinsic (clang exposes no builtin), so the compiler's hazard
+// recognizer sees it: a v_cmp that writes the SGPR pair needs one wait state before a v_writelane
+// reads it, which an inline-asm writelane silently violates (stale ballot bits).
+__device__ int amdgcn_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 template <int L>
 __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
 {
-    asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(acc) : "s"(v), "i"(L));
+    acc = (uint32_t)amdgcn_writelane((int)v, L, (int)acc);
 }
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ bool all_lanes(bool p) { return ballot(p) == ballot(true); }
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m)
+// Maximum of a 64-bit value over the wave without divergent control flow (readlane into SGPRs).
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 {
-    const int lo = __shfl_xor((int)(uint32_t)v, m, 64);
-    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
+    uint64_t best = 0;
+    for (int l = 0; l < kWave; ++l)
+    {
+        const uint64_t x = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane(lo, l);
+        best = x > best ? x : best;
+    }
+    return best;
 }
 
 __device__ __forceinline__ uint64_t load_granule(const uint64_t *p)
@@ -108,6 +121,7 @@ struct FillArgs {
     int32_t A;
     uint32_t epoch;
     int32_t key_bits;
+    uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
 };
 
 // Waits until lanes 0..U-1 hold the granules of columns base+1 .. base+U of the strip above.
@@ -118,20 +132,26 @@ __device__ __forceinline__ bool wait_feed(const FillArgs &a, const uint64_t *bin
 {
     const bool need = lane < U && base + lane < n;
     bool ready = !need || (uint32_t)(v >> 32) == a.epoch;
-    if (__all(ready)) return true;
+    if (all_lanes(ready)) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spin = 0;; ++spin)
     {
         __builtin_amdgcn_s_sleep(2);
         if (!ready) v = load_granule(bin + base + lane);
         ready = !need || (uint32_t)(v >> 32) == a.epoch;
-        if (__all(ready)) return true;
+        if (all_lanes(ready)) return true;
         if ((spin & 63) == 63)
         {
             // 100 MHz constant clock: give up after ~20 s, and whenever another wave gave up.
-            const bool late = __builtin_amdgcn_s_memrealtime() - t0 > 2000000000ull;
-            if (late) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return false;
+            const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+#ifdef SA_TB_DEBUG
+            if (lane == 0 && (spin & 1048575) == 1048575)
+                printf("wait base=%d n=%d v=%llx epoch=%u t=%llu\n", base, n, (unsigned long long)v, a.epoch,
+                       (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
+#endif
+            if (late && lane == 0) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int aborted = uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (aborted || late) return false;
         }
     }
 }
@@ -269,7 +289,7 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
     if (hasPrev)
     {
         uint64_t v = (lane < U && lane < n) ? load_granule(bin + lane) : 0;
-        ok = wait_feed<U>(a, bin, 0, n, lane, v);
+        ok = uniform(wait_feed<U>(a, bin, 0, n, lane, v)) != 0;
         FB = (int)(uint32_t)v;
     }
     int published = 0;
@@ -328,7 +348,7 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
         }
         if (hasPrev && s1 < nSteps)
         {
-            ok = wait_feed<U>(a, bin, s1, n, lane, gn);
+            ok = uniform(wait_feed<U>(a, bin, s1, n, lane, gn)) != 0;
             FB = (int)(uint32_t)gn;
         }
         sfor<U>([&](auto Qc) {
@@ -336,13 +356,12 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
             T[q] = Tn[q];
         });
     }
-    if (!ok) return;
     if constexpr (LOCAL)
     {
-        for (int off = 32; off > 0; off >>= 1) lbest = max(lbest, shfl_xor_u64(lbest, off));
-        if (lane == 0) a.strip_best[idx] = lbest;
+        const uint64_t wbest = wave_max_u64(lbest);
+        if (ok && lane == 0) a.strip_best[idx] = wbest;
     }
-    else
+    else if (ok)
     {
         const int rm = m - sd.row0;  // strip-relative row of the last DP row
         if (rm >= 0 && rm < kWave * R && lane == rm / R)
@@ -369,12 +388,12 @@ __global__ __launch_bounds__(64) void fill_kernel(FillArgs a)
     }
     while (true)
     {
-        uint32_t idx = 0;
-        if (lane == 0) idx = atomicAdd(&a.ctrl->queue_head, 1u);
-        idx = __shfl(idx, 0, 64);
-        if (idx >= (uint32_t)a.num_strips) break;
-        if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-        process_strip<R, LOCAL, PACKED>(a, ldsS, (int)idx, lane);
+        int idx = 0;
+        if (lane == 0) idx = (int)atomicAdd(&a.ctrl->queue_head, 1u);
+        idx = __builtin_amdgcn_readlane(idx, 0);
+        if (idx >= a.num_strips) break;
+        if (uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
+        process_strip<R, LOCAL, PACKED>(a, ldsS, idx, lane);
     }
 }
 
@@ -436,7 +455,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
     {
         uint64_t k = 0;
         for (int s = lane; s < pd.num_strips; s += kWave) k = max(k, a.strip_best[pd.first_strip + s]);
-        for (int off = 32; off > 0; off >>= 1) k = max(k, shfl_xor_u64(k, off));
+        k = wave_max_u64(k);
         const int H = (int)(k >> (2 * kKeyRowBits));
         if (H > 0)
         {
@@ -467,6 +486,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
             const StripDesc sd = a.strips[pd.first_strip + b];
             const uint4 *src = a.masks + sd.mask_off + (uint64_t)wlo * R;
             const int cnt = (whi - wlo + 1) * R;
+#ifdef SA_TB_DEBUG
+            if (lane == 0) printf("reload i=%d j=%d b=%d k=%d rho=%d s=%d wlo=%d whi=%d off=%llu cnt=%d nsteps=%d\n", ci, cj, b, k, rho, s, wlo, whi, (unsigned long long)sd.mask_off, cnt, sd.nsteps);
+#endif
             for (int e = lane; e < cnt; e += kWave) win[e] = src[e];
             __syncthreads();
         }
@@ -491,6 +513,10 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
             const int d = j == 0 ? kTop : (i == 0 ? kLeft : code_at(i, j));
             const int tt = d == kDiag || d == kLeft;
             const int tp = d == kDiag || d == kTop;
+#ifdef SA_TB_DEBUG
+            if (lane == 0 && len >= n + m) printf("BAD len=%d i=%d j=%d d=%d\n", len, i, j, d);
+            if (lane == 0 && len < 4000) printf("mv %d %d %d %d\n", len, i, j, d);
+#endif
             if (lane == 0) ops[len] = (uint8_t)d;
             ++len;
             ti = max(0, ti - tt);
@@ -511,6 +537,10 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
             if (d == kStop) break;
             const int tt = d == kDiag || d == kLeft;
             const int tp = d == kDiag || d == kTop;
+#ifdef SA_TB_DEBUG
+            if (lane == 0 && len >= n + m) printf("BAD len=%d i=%d j=%d d=%d\n", len, i, j, d);
+            if (lane == 0 && len < 4000) printf("mv %d %d %d %d\n", len, i, j, d);
+#endif
             if (lane == 0) ops[len] = (uint8_t)d;
             ++len;
             i -= tp;
@@ -552,11 +582,22 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
     char *ot = a.out_text + pd.out_off;
     char *op = a.out_pattern + pd.out_off;
     int xt = ti0 - bt, xp = pi0 - bp;
+#ifdef SA_TB_DEBUG
+    if (c0 < c1) printf("letters lane=%d c0=%d c1=%d len=%d xt=%d xp=%d ti0=%d pi0=%d\n", lane, c0, c1, len, xt, xp, ti0, pi0);
+#endif
     for (int t = c0; t < c1; ++t)
     {
         const int d = ops[t];
         const int tt = d == kDiag || d == kLeft;
         const int tp = d == kDiag || d == kTop;
+#ifdef SA_TB_DEBUG
+        if ((tt && (xt < 0 || xt >= n)) || (tp && (xp < 0 || xp >= m)) || d > 3)
+        {
+            printf("BAD letter lane=%d t=%d d=%d xt=%d xp=%d n=%d m=%d len=%d\n", lane, t, d, xt, xp, n, m, len);
+            xt -= tt; xp -= tp;
+            continue;
+        }
+#endif
         ot[len - 1 - t] = tt ? alpha[(int)a.text[pd.text_off + xt]] : GAPC;
         op[len - 1 - t] = tp ? alpha[(int)a.pattern[pd.pattern_off + xp]] : GAPC;
         xt -= tt;
@@ -580,6 +621,11 @@ __global__ void selftest_kernel(int *out)
     writelane<6>(acc, (uint32_t)(b >> 32));
     out[3 * 64 + lane] = (int)acc;
     out[4 * 64 + lane] = __builtin_amdgcn_sbfe(0x18F70A05, 8 * (lane & 3), 8);  // 5, 10, -9, 24
+    // constant 100 MHz clock used by the hand-off timeout must advance
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 2000; ++k) __builtin_amdgcn_s_sleep(10);
+    const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+    out[5 * 64 + lane] = (int)(t1 - t0);
 }
 
 }  // namespace sa
@@ -604,6 +650,18 @@ int fail(int code, const std::string &msg)
         hipError_t e_ = (expr);                                                              \
         if (e_ != hipSuccess) return fail(SA_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
+
+// SA_DEBUG_SYNC=1: synchronise and check after every launch (names the failing kernel).
+int debug_sync(hipStream_t st, const char *what)
+{
+    static const bool on = std::getenv("SA_DEBUG_SYNC") != nullptr;
+    if (!on) return SA_OK;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e != hipSuccess) return fail(SA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    std::fprintf(stderr, "[sa debug] %s ok\n", what);
+    return SA_OK;
+}
 
 template <typename T>
 int dmalloc(T **p, size_t bytes)
@@ -925,6 +983,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
                                pl->d_pairs + y0, pl->d_codes, pl->A, pl->packed ? 8 : 1);
         }
         HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "encode_text_kernel")) return rc;
     }
     const int ns = (int)pl->strips.size();
     if (ns > 0)
@@ -946,9 +1005,15 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.A = pl->A;
         a.epoch = pl->epoch;
         a.key_bits = pl->key_bits;
+        {
+            const char *e = std::getenv("SA_HANDOFF_TIMEOUT_S");
+            const double secs = e ? std::atof(e) : 20.0;
+            a.timeout_ticks = (uint64_t)(secs * 1e8);
+        }
         const int grid = std::min(ns, std::max(1, pl->num_cu) * 8);
         launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->packed, grid, st);
         HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "fill_kernel")) return rc;
     }
     pl->filled = true;
     HIP_TRY(hipSetDevice(cur));
@@ -982,6 +1047,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     std::memcpy(a.alphabet, pl->alphabet, 33);
     launch_tb(pl->R, a, np, st);
     HIP_TRY(hipGetLastError());
+    if (int rc = debug_sync(st, "traceback_kernel")) return rc;
     HIP_TRY(hipSetDevice(cur));
     return SA_OK;
 }
@@ -1022,6 +1088,43 @@ int sa_plan_fetch_alignment(sa_plan *pl, int64_t index, char *at, char *ap, uint
         HIP_TRY(hipStreamSynchronize(st));
     }
     HIP_TRY(hipSetDevice(cur));
+    return SA_OK;
+}
+
+int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *stream)
+{
+    if (!pl || !M || index < 0 || index >= (int64_t)pl->pairs.size()) return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: bad argument");
+    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    const PairDesc &pd = pl->pairs[index];
+    const uint64_t n = pd.text_len, m = pd.pattern_len, cols = n + 1;
+    const bool local = pl->mode == SA_LOCAL;
+    for (uint64_t j = 0; j < cols; ++j) M[j] = local ? 3 : 0;          // row 0: STOP / LEFT
+    for (uint64_t i = 1; i <= m; ++i) M[i * cols] = local ? 3 : 2;     // column 0: STOP / TOP
+    if (pd.num_strips == 0) return SA_OK;
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    HIP_TRY(hipSetDevice(pl->device));
+    const StripDesc &first = pl->strips[pd.first_strip];
+    const StripDesc &last = pl->strips[pd.first_strip + pd.num_strips - 1];
+    const uint64_t e0 = first.mask_off, e1 = last.mask_off + (uint64_t)last.nsteps * pl->R;
+    std::vector<uint32_t> h((e1 - e0) * 4);
+    HIP_TRY(hipMemcpyAsync(h.data(), pl->d_masks + e0 * 4, h.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipSetDevice(cur));
+    const int R = pl->R, RB = kWave * R;
+    for (uint64_t i = 1; i <= m; ++i)
+    {
+        const uint64_t b = (i - 1) / RB, il = (i - 1) % RB, k = il / R, rho = il % R;
+        const StripDesc &sd = pl->strips[pd.first_strip + b];
+        for (uint64_t j = 1; j <= n; ++j)
+        {
+            const uint64_t e = (sd.mask_off - e0) + (j - 1 + k) * R + rho;
+            const uint32_t *w = &h[e * 4];
+            const uint32_t b0 = (w[k < 32 ? 0 : 1] >> (k & 31)) & 1u;
+            const uint32_t b1 = (w[k < 32 ? 2 : 3] >> (k & 31)) & 1u;
+            M[i * cols + j] = (uint8_t)(b0 | (b1 << 1));
+        }
+    }
     return SA_OK;
 }
 
@@ -1096,9 +1199,9 @@ int sa_selftest(int device)
     HIP_TRY(hipGetDevice(&cur));
     HIP_TRY(hipSetDevice(device));
     int *d = nullptr;
-    HIP_TRY(hipMalloc(&d, 5 * 64 * sizeof(int)));
+    HIP_TRY(hipMalloc(&d, 6 * 64 * sizeof(int)));
     hipLaunchKernelGGL(selftest_kernel, dim3(1), dim3(64), 0, 0, d);
-    std::vector<int> h(5 * 64);
+    std::vector<int> h(6 * 64);
     HIP_TRY(hipMemcpy(h.data(), d, h.size() * sizeof(int), hipMemcpyDeviceToHost));
     HIP_TRY(hipFree(d));
     HIP_TRY(hipSetDevice(cur));
@@ -1114,6 +1217,7 @@ int sa_selftest(int device)
         const int wl = l == 5 ? (int)(uint32_t)b : (l == 6 ? (int)(uint32_t)(b >> 32) : 0);
         if (h[192 + l] != wl) return fail(SA_ERR_UNSUPPORTED, "ballot/writelane mismatch at lane " + std::to_string(l));
         if (h[256 + l] != sbfe[l & 3]) return fail(SA_ERR_UNSUPPORTED, "v_bfe_i32 mismatch at lane " + std::to_string(l));
+        if (h[320 + l] <= 0) return fail(SA_ERR_UNSUPPORTED, "s_memrealtime does not advance (" + std::to_string(h[320 + l]) + ")");
     }
     return SA_OK;
 }

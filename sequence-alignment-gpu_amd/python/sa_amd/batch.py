@@ -49,5 +49,8 @@ class DeviceBatch:
     def alignment(self, i: int) -> tuple[str, str]:
         return self.plan.alignment(i, self.stream())
 
+    def directions(self, i: int):
+        return self.plan.directions(i, self.stream())
+
     def close(self) -> None:
         self.plan.close()

@@ -20,7 +20,7 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 # Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
-           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest")
+           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions")
 
 
 class SaParams(ctypes.Structure):
@@ -47,6 +47,13 @@ class SaError(RuntimeError):
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"HIP engine not built: {LIB_PATH} is missing (run __graft_entry__.build())")
+    # One HIP runtime per process: torch ships its own libamdhip64 (soname libamdhip64.so.7, but its
+    # libraries NEED "libamdhip64.so"). Loaded first, torch's runtime also satisfies our NEEDED
+    # libamdhip64.so.7; loaded after us it would start a second runtime that sees no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, I, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64
     L.sa_align_pair.argtypes = [ctypes.POINTER(SaParams), P, U64, P, U64, I, ctypes.POINTER(SaResult), P, P, U64,
@@ -60,6 +67,7 @@ def _load():
     L.sa_plan_fetch_alignment.argtypes = [P, ctypes.c_int64, P, P, U64, P]
     L.sa_plan_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    L.sa_plan_fetch_directions.argtypes = [P, ctypes.c_int64, P, P]
     L.sa_plan_device_results.argtypes = [P]
     L.sa_plan_device_results.restype = P
     L.sa_device_count.argtypes = [ctypes.POINTER(I)]
@@ -149,6 +157,13 @@ class Plan:
         _check(lib.sa_plan_fetch_results(self.handle, out, stream))
         return [{"score": r.score, "num_bytes": r.num_alignment_bytes, "start_text": r.start_text,
                  "start_pattern": r.start_pattern} for r in out[: self.num_pairs]]
+
+    def directions(self, index: int, stream: int | None = None) -> np.ndarray:
+        """Decoded (m+1)x(n+1) DIRECTION matrix of pair `index` (reference layout, for verification)."""
+        n, m = self.pairs[index][1], self.pairs[index][3]
+        M = np.empty((m + 1) * (n + 1), dtype=np.uint8)
+        _check(lib.sa_plan_fetch_directions(self.handle, index, M.ctypes.data, stream))
+        return M
 
     def alignment(self, index: int, stream: int | None = None) -> tuple[str, str]:
         cap = max(1, self.pairs[index][1] + self.pairs[index][3])

@@ -172,3 +172,23 @@ def test_batch_plan_config5(eng, golden):
     res2 = b.run()
     assert res2 == res
     b.close()
+
+
+@pytest.mark.parametrize("rows_per_lane", [1, 2, 4, 8, 16, 32])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane):
+    """The fill alone, cell by cell: the engine's DIRECTION matrix (decoded from its bit-planes) equals
+    the reference's (m+1)x(n+1) byte matrix M (alignSequenceCPU.cpp:116-284) on every cell."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    for k, (n, m) in enumerate([(1500, 1400), (700, 700), (130, 66)]):
+        t = synthetic.random_sequence(500 + k, n, 4)
+        p = synthetic.mutate(t, 600 + k, 4, m)
+        b = DeviceBatch(mode, S, 5, [t], [p], rows_per_lane=rows_per_lane)
+        b.fill()
+        got = b.directions(0)
+        exp = np.empty((m + 1) * (n + 1), np.uint8)
+        oracle.fill_only(mode, t, p, S, 5, exp)
+        bad = int((got != exp).sum())
+        b.close()
+        assert bad == 0, (n, m, bad)
