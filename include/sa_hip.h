@@ -90,7 +90,8 @@ int sa_plan_create(const sa_params *params, const sa_pair *pairs, int64_t num_pa
                    sa_plan **out);
 int sa_plan_destroy(sa_plan *plan);
 
-/* Enqueue the DP fill of every pair on `stream` (a hipStream_t; NULL = the plan's own stream).
+/* Enqueue the DP fill of every pair on `stream` (a hipStream_t; NULL = the HIP null stream, which is
+ * also what torch.cuda's default stream handle 0 denotes).
  * d_text / d_pattern are device arenas of alphabet indices addressed by sa_pair offsets. */
 int sa_plan_fill(sa_plan *plan, const void *d_text, const void *d_pattern, void *stream);
 

@@ -960,7 +960,7 @@ int sa_plan_destroy(sa_plan *plan)
 int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *stream)
 {
     if (!pl || (!pl->pairs.empty() && (!d_text || !d_pattern))) return fail(SA_ERR_INVALID, "sa_plan_fill: null argument");
-    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     HIP_TRY(hipSetDevice(pl->device));
@@ -1023,7 +1023,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
 int sa_plan_traceback(sa_plan *pl, void *stream)
 {
     if (!pl || !pl->filled) return fail(SA_ERR_INVALID, "sa_plan_traceback: plan not filled");
-    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     const int np = (int)pl->pairs.size();
     if (np == 0) return SA_OK;
     int cur = 0;
@@ -1055,7 +1055,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
 int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
 {
     if (!pl || !out) return fail(SA_ERR_INVALID, "sa_plan_fetch_results: null argument");
-    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     HIP_TRY(hipSetDevice(pl->device));
@@ -1072,7 +1072,7 @@ int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
 int sa_plan_fetch_alignment(sa_plan *pl, int64_t index, char *at, char *ap, uint64_t cap, void *stream)
 {
     if (!pl || index < 0 || index >= (int64_t)pl->pairs.size()) return fail(SA_ERR_INVALID, "sa_plan_fetch_alignment: bad index");
-    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     HIP_TRY(hipSetDevice(pl->device));
@@ -1094,7 +1094,7 @@ int sa_plan_fetch_alignment(sa_plan *pl, int64_t index, char *at, char *ap, uint
 int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *stream)
 {
     if (!pl || !M || index < 0 || index >= (int64_t)pl->pairs.size()) return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: bad argument");
-    hipStream_t st = stream ? (hipStream_t)stream : pl->own;
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     const PairDesc &pd = pl->pairs[index];
     const uint64_t n = pd.text_len, m = pd.pattern_len, cols = n + 1;
     const bool local = pl->mode == SA_LOCAL;
