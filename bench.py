@@ -181,7 +181,8 @@ def main():
         avg_ms = float(np.mean(launch_ms))
         bytes_per_launch = float(cells_rank)  # algorithmic: 1 DIRECTION byte per cell
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        traffic = load_traffic(workload["workload"])
+        tr = load_traffic(workload["workload"])
+        traffic = tr["bytes_per_launch"] if tr else None
         out = {
             "metric": "GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA NW",
             "value": round(value, 3),
@@ -198,7 +199,9 @@ def main():
             "config": dict(workload, rows_per_lane=info["rows_per_lane"], strips_per_gpu=info["num_strips"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic},
+                         "traffic": traffic,
+                         "traffic_note": (tr["source"] + "; physical HBM bytes per fill launch (direction bit-planes "
+                                          "are 2 bits/cell, so traffic < algorithmic 1 B/cell)") if tr else None},
             "fill_ms_per_launch": {"mean": round(avg_ms, 4), "min": round(min(launch_ms), 4),
                                    "median": round(float(np.median(launch_ms)), 4)},
             "gcups_best_launch": round(cells_rank / (min(launch_ms) * 1e-3) / 1e9 * world, 3),

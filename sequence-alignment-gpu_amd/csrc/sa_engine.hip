@@ -66,8 +66,33 @@ __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
     acc = (uint32_t)amdgcn_writelane((int)v, L, (int)acc);
 }
 
+// Direction planes go to memory straight from the SGPRs the ballots produced: one scalar-pipe
+// s_store_dwordx4 per (step,row) slot = {plane0, plane1} (no VALU work). The scalar data cache is
+// written back with s_dcache_wb at the end of every strip. SA_VECTOR_MASK_STORE selects the
+// alternative (v_writelane into a VGPR per 16 slots + one coalesced global store).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <int OFF>
+__device__ __forceinline__ void sstore_slot(uint32_t *base, uint64_t p0, uint64_t p1)
+{
+    const u32x4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+    asm volatile("s_store_dwordx4 %0, %1, %2\n\ts_nop 0" ::"s"(v), "s"(base), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ void sstore_flush()
+{
+    __builtin_amdgcn_s_dcache_wb();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+template <typename T>
+__device__ __forceinline__ T *uniform_ptr(T *p)
+{
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return (T *)(((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ bool all_lanes(bool p) { return ballot(p) == ballot(true); }
 
 // Maximum of a 64-bit value over the wave without divergent control flow (readlane into SGPRs).
@@ -161,7 +186,7 @@ template <int R, bool LOCAL, bool PACKED, bool RAMP>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
                                          int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &FB,
-                                         int &O, uint32_t (&acc)[Cfg<R>::NACC])
+                                         int &O, uint32_t (&acc)[Cfg<R>::NACC], uint32_t *mbase)
 {
     constexpr int U = Cfg<R>::U;
     sfor<U>([&](auto Qc) {
@@ -233,11 +258,16 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 p1 = (tp & ~d) | z;
             }
             constexpr int slot = q * R + rho;
+#ifdef SA_VECTOR_MASK_STORE
             constexpr int ai = slot / 16, l = (slot % 16) * 4;
             writelane<l + 0>(acc[ai], (uint32_t)p0);
             writelane<l + 1>(acc[ai], (uint32_t)(p0 >> 32));
             writelane<l + 2>(acc[ai], (uint32_t)p1);
             writelane<l + 3>(acc[ai], (uint32_t)(p1 >> 32));
+#else
+            (void)acc;
+            sstore_slot<slot * 16>(mbase, p0, p1);
+#endif
         });
         // collect the strip's bottom row: lane 63 appends, everything else moves down one lane
         O = dpp_shl1(F[R - 1], O);
@@ -305,15 +335,18 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
         if (hasPrev && s1 < nSteps && lane < U && s1 + lane < n) gn = load_granule(bin + s1 + lane);
         uint32_t acc[NACC];
         sfor<NACC>([&](auto Cc) { acc[decltype(Cc)::value] = 0; });
+        uint32_t *mbase = uniform_ptr(mk + (size_t)s0 * R * 4);  // this body's first direction entry
         const bool steady = (s0 >= kWave - 1) && (s1 <= n);
         if (steady)
-            run_body<R, LOCAL, PACKED, false>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc);
+            run_body<R, LOCAL, PACKED, false>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
         else
-            run_body<R, LOCAL, PACKED, true>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc);
+            run_body<R, LOCAL, PACKED, true>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
+#ifdef SA_VECTOR_MASK_STORE
         sfor<NACC>([&](auto Cc) {
             constexpr int c = decltype(Cc)::value;
             mk[((size_t)s0 * R + c * 16) * 4 + lane] = acc[c];
         });
+#endif
         if (hasNext && (((s1 & 15) == 0) || s1 >= nSteps))
         {
             const int sl = s1 - 1;
@@ -356,6 +389,9 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
             T[q] = Tn[q];
         });
     }
+#ifndef SA_VECTOR_MASK_STORE
+    sstore_flush();
+#endif
     if constexpr (LOCAL)
     {
         const uint64_t wbest = wave_max_u64(lbest);
