@@ -213,7 +213,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             if args.workload == "batch":
-                out["cpu_baseline"] = cpu_baseline("global", 2048, args.cpu_rows or 2048 * 16, seeds=(1000, 1001))
+                # 512 pairs' worth of cells (2048 columns x 2^20 rows, one tall fill), ~2-5 s on one core
+                out["cpu_baseline"] = cpu_baseline("global", 2048, args.cpu_rows or 2048 * 512, seeds=(1000, 1001))
             else:
                 out["cpu_baseline"] = cpu_baseline("global" if args.workload == "headline" else "local",
                                                    args.size, args.cpu_rows or args.size)
