@@ -96,11 +96,12 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
-    from sa_amd import engine, synthetic
+    from sa_amd import distributed, synthetic
     from sa_amd.batch import DeviceBatch
 
     S = synthetic.blast_matrix()
     gap = 5
+    npairs = 1
     if args.workload in ("headline", "local"):
         n = m = args.size
         mode = 0 if args.workload == "headline" else 1
@@ -114,7 +115,7 @@ def main():
                     "parallelism": f"replicas{world}"}
     else:
         npairs, L = 4096, 2048
-        mine = list(range(rank, npairs, world))
+        mine = distributed.shard(npairs, world, rank)
         texts = [synthetic.random_sequence(1000 + 2 * i, L, 4) for i in mine]
         pats = [synthetic.random_sequence(1001 + 2 * i, L, 4) for i in mine]
         job = DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)
@@ -125,10 +126,17 @@ def main():
     info = job.plan.info()
     stream = torch.cuda.current_stream(local)
 
+    dev = torch.device("cuda", local)
+
     def step():
         job.fill()
         if args.workload == "batch":
+            # whole batch job per step: fill + traceback of this rank's pairs, results to host, and
+            # the path's exchange step — every rank's results gathered to rank 0 over RCCL (xGMI)
             job.traceback()
+            r = job.results()
+            if world > 1:
+                distributed.gather_results(r, npairs, world, rank, dev)
 
     for _ in range(args.warmup):
         step()
@@ -168,13 +176,9 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tmax = float(tt.item())
         if args.workload == "batch":
-            # the batch path's exchange step: per-rank score shards gathered to rank 0 over RCCL
-            mine_t = torch.tensor(scores, dtype=torch.int32, device="cuda")
-            width = (4096 + world - 1) // world
-            pad = torch.full((width,), -2**31, dtype=torch.int32, device="cuda")
-            pad[: len(scores)] = mine_t
-            gathered = [torch.empty_like(pad) for _ in range(world)] if rank == 0 else None
-            dist.gather(pad, gathered, dst=0)
+            allres = distributed.gather_results(res, npairs, world, rank, dev)
+            if rank == 0:
+                scores = [r["score"] for r in allres]
     cells_total = cells_rank * world
     value = cells_total * args.steps / tmax / 1e9
     if rank == 0:

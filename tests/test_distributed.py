@@ -1,0 +1,83 @@
+"""CPU, world_size 2 over gloo: the batch path's sharding (pair i -> rank i mod world) and the
+result gather to rank 0 (sa_amd.distributed) reassemble exactly the single-process results. The
+per-pair computation here is the oracle (CPU test stand-in for the GPU engine; the GPU path of the
+same gather is exercised by bench.py --workload batch on the box)."""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _pairs(num):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+    from sa_amd import synthetic
+    out = []
+    for i in range(num):
+        t = synthetic.random_sequence(1000 + 2 * i, 96 + 7 * i, 4)
+        p = synthetic.random_sequence(1001 + 2 * i, 80 + 5 * i, 4)
+        out.append((t, p))
+    return out
+
+
+def _worker(rank, world, port, num, mode, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch.distributed as dist
+
+    import oracle
+    from sa_amd import distributed, synthetic
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pairs = _pairs(num)
+    S = synthetic.blast_matrix()
+    mine = distributed.shard(num, world, rank)
+    res = []
+    for i in mine:
+        r = oracle.align(mode, pairs[i][0], pairs[i][1], S, 5)
+        res.append({k: r[k] for k in distributed.FIELDS})
+    out = distributed.gather_results(res, num, world, rank, "cpu")
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_sharded_batch_gather_world2(mode):
+    num = 13  # uneven split on purpose
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, num, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    from sa_amd import distributed, synthetic
+    S = synthetic.blast_matrix()
+    pairs = _pairs(num)
+    for i in range(num):
+        r = oracle.align(mode, pairs[i][0], pairs[i][1], S, 5)
+        assert got[i] == {k: r[k] for k in distributed.FIELDS}, i
+    # the deal is round-robin and covers every pair exactly once
+    assert sorted(distributed.shard(num, 2, 0) + distributed.shard(num, 2, 1)) == list(range(num))
