@@ -131,7 +131,7 @@ struct Cfg {
 
 struct FillArgs {
     const int8_t *pattern;      // device pattern arena (alphabet indices)
-    const int8_t *codes;        // padded text codes (8*c for the packed profile, c otherwise)
+    const int32_t *codes;       // padded text codes, one dword per letter (8*c packed profile, c otherwise)
     const StripDesc *strips;
     const PairDesc *pairs;
     const int32_t *prof_tab;    // packed profile: one word per pattern letter (A <= 4)
@@ -142,42 +142,60 @@ struct FillArgs {
     int32_t *pair_score;        // global: H[m][n] per pair
     Control *ctrl;
     int32_t num_strips;
+    int32_t num_groups;         // ceil(num_strips / W)
     int32_t gap;
     int32_t A;
     uint32_t epoch;
     int32_t key_bits;
     uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
+    uint64_t *timeline;         // debug (SA_TIMELINE): per strip {start, fed, end, hw id}, or null
 };
 
-// Waits until lanes 0..U-1 hold the granules of columns base+1 .. base+U of the strip above.
-// `v` is a value already loaded (prefetched); returns false if the launch is being aborted.
-template <int U>
-__device__ __forceinline__ bool wait_feed(const FillArgs &a, const uint64_t *bin, int base, int n,
-                                          int lane, uint64_t &v)
+// Work unit of the fill kernel: a GROUP of W consecutive strips. A workgroup has W compute waves
+// (one strip each) and one I/O wave. Compute waves only ever exchange rows through LDS rings:
+// ring[w] feeds compute wave w; wave w writes its bottom row into ring[w+1]. The I/O wave links the
+// group to its neighbours in global memory: it copies the previous group's granules into ring[0]
+// and drains ring[W] into granules for the next group. Keeping every global store and poll out of
+// the compute waves matters: on gfx9 a store shares the vmcnt counter with the text-code loads, and
+// a cross-XCD (sc1) store takes ~0.7 us to retire, which would stall the next load wait.
+typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, never flat
+constexpr int kRing = 2048;        // ring entries (columns), power of two
+constexpr int kRingMask = kRing - 1;
+constexpr int kMaxWaves = 8;       // compute waves per workgroup
+
+struct GroupHdr {
+    int S[32 * 32];                // generic score table (A <= 32)
+    int prog[kMaxWaves + 1];       // prog[w]: columns published into ring[w]
+    int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
+    int group;                     // group index taken from the queue
+    int pad[1];
+};
+__host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + (size_t)(W + 1) * kRing * 4; }
+
+// Bounded-spin helper, called every few polls: false (and the abort word raised) after the
+// timeout, or as soon as another wave has given up.
+__device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int lane)
 {
-    const bool need = lane < U && base + lane < n;
-    bool ready = !need || (uint32_t)(v >> 32) == a.epoch;
-    if (all_lanes(ready)) return true;
+    // 100 MHz constant clock
+    const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+    if (late && lane == 0) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int aborted = uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return !(aborted || late);
+}
+
+// Waits until the producer wave has published columns 1..need into the ring (LDS progress word).
+__device__ __forceinline__ bool wait_ring(const FillArgs &a, volatile lds_int *prog, int need, int &avail, int lane)
+{
+    if (avail >= need) return true;
+    avail = uniform(*prog);
+    if (avail >= need) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t spin = 0;; ++spin)
+    for (uint32_t spin = 1;; ++spin)
     {
-        __builtin_amdgcn_s_sleep(2);
-        if (!ready) v = load_granule(bin + base + lane);
-        ready = !need || (uint32_t)(v >> 32) == a.epoch;
-        if (all_lanes(ready)) return true;
-        if ((spin & 63) == 63)
-        {
-            // 100 MHz constant clock: give up after ~20 s, and whenever another wave gave up.
-            const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
-#ifdef SA_TB_DEBUG
-            if (lane == 0 && (spin & 1048575) == 1048575)
-                printf("wait base=%d n=%d v=%llx epoch=%u t=%llu\n", base, n, (unsigned long long)v, a.epoch,
-                       (unsigned long long)(__builtin_amdgcn_s_memrealtime() - t0));
-#endif
-            if (late && lane == 0) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int aborted = uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            if (aborted || late) return false;
-        }
+        __builtin_amdgcn_s_sleep(1);
+        avail = uniform(*prog);
+        if (avail >= need) return true;
+        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
     }
 }
 
@@ -275,7 +293,7 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
 }
 
 template <int R, bool LOCAL, bool PACKED>
-__device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, int idx, int lane)
+__device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
     constexpr int NACC = Cfg<R>::NACC;
@@ -293,13 +311,17 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
         c = min(max(c, 0), a.A - 1);
         prof[rho] = PACKED ? a.prof_tab[c] : c * a.A;
     });
-    const int8_t *codes = a.codes + pd.code_off + kPad;
+    const int32_t *codes = a.codes + pd.code_off + kPad;
     const bool hasPrev = (sd.flags & kHasPrev) != 0;
     const bool hasNext = (sd.flags & kHasNext) != 0;
-    const uint64_t *bin = a.bnd + sd.bnd_in;
-    uint64_t *bout = a.bnd + sd.bnd_out;
+    volatile lds_int *rin = (volatile lds_int *)(rings + w * kRing);
+    volatile lds_int *rout = (volatile lds_int *)(rings + (w + 1) * kRing);
+    volatile lds_int *progIn = (volatile lds_int *)&H.prog[w];
+    volatile lds_int *consIn = (volatile lds_int *)&H.cons[w];
+    volatile lds_int *progOut = (volatile lds_int *)&H.prog[w + 1];
+    volatile lds_int *consOut = (volatile lds_int *)&H.cons[w + 1];
     uint32_t *mk = a.masks + sd.mask_off * 4;
-    const int nSteps = sd.nsteps;
+    const int nSteps = sd.nsteps;  // a multiple of 2U
 
     // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
     int F[R], G[R], best[R];
@@ -310,50 +332,68 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
         best[rho] = 0;
     });
     int upPrev = 0, FB = 0, O = 0;
-    int T[U], Tn[U];
-    sfor<U>([&](auto Qc) {
-        constexpr int q = decltype(Qc)::value;
-        T[q] = codes[q - lane];
-    });
+    // text codes, double-buffered across the two bodies of one loop trip (no register copies);
+    // lane k at step s needs the code of column s-k+1, i.e. codes[s - k]
+    int TA[U], TB[U];
+    auto load_codes = [&](int s0, int (&dst)[U]) {
+        typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+        sfor<U / 4>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value * 4;
+            const i32x4u v = *(const i32x4u *)(codes + s0 + q - lane);
+            dst[q] = v.x;
+            dst[q + 1] = v.y;
+            dst[q + 2] = v.z;
+            dst[q + 3] = v.w;
+        });
+    };
+    const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    load_codes(0, TA);
     bool ok = true;
-    if (hasPrev)
-    {
-        uint64_t v = (lane < U && lane < n) ? load_granule(bin + lane) : 0;
-        ok = uniform(wait_feed<U>(a, bin, 0, n, lane, v)) != 0;
-        FB = (int)(uint32_t)v;
-    }
+    int avail = 0;       // columns known to be in rin
+    int consKnown = 0;   // columns the consumer of rout is known to have read
+    // lanes 0..U-1 take the bottom values of columns base+1 .. base+U of the strip above
+    auto feed = [&](int base) -> bool {
+        if (!hasPrev) return true;  // row 0 boundary: FB stays 0
+        if (!wait_ring(a, progIn, min(n, base + U), avail, lane)) return false;
+        FB = (lane < U && base + lane < n) ? rin[(base + lane) & kRingMask] : 0;
+        if (lane == 0) *consIn = base + U;
+        return true;
+    };
+    ok = feed(0);
+    const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     int published = 0;
     uint64_t lbest = 0;
-    for (int s0 = 0; ok && s0 < nSteps; s0 += U)
-    {
+    auto body = [&](int s0, int (&T)[U], int (&Tn)[U]) -> bool {
         const int s1 = s0 + U;
-        sfor<U>([&](auto Qc) {
-            constexpr int q = decltype(Qc)::value;
-            Tn[q] = codes[s1 + q - lane];
-        });
-        uint64_t gn = 0;
-        if (hasPrev && s1 < nSteps && lane < U && s1 + lane < n) gn = load_granule(bin + s1 + lane);
+        load_codes(s1, Tn);  // prefetch one body ahead
         uint32_t acc[NACC];
         sfor<NACC>([&](auto Cc) { acc[decltype(Cc)::value] = 0; });
         uint32_t *mbase = uniform_ptr(mk + (size_t)s0 * R * 4);  // this body's first direction entry
         const bool steady = (s0 >= kWave - 1) && (s1 <= n);
         if (steady)
-            run_body<R, LOCAL, PACKED, false>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
+            run_body<R, LOCAL, PACKED, false>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
         else
-            run_body<R, LOCAL, PACKED, true>(ldsS, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
-#ifdef SA_VECTOR_MASK_STORE
-        sfor<NACC>([&](auto Cc) {
-            constexpr int c = decltype(Cc)::value;
-            mk[((size_t)s0 * R + c * 16) * 4 + lane] = acc[c];
-        });
-#endif
-        if (hasNext && (((s1 & 15) == 0) || s1 >= nSteps))
+            run_body<R, LOCAL, PACKED, true>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
+        if (hasNext)
         {
-            const int sl = s1 - 1;
-            const int col = sl - 125 + lane;  // column whose bottom value O holds in this lane
-            if (lane >= 48 && col >= 1 && col <= n && col > published)
-                store_granule(bout + col - 1, ((uint64_t)a.epoch << 32) | (uint32_t)O);
-            published = min(n, max(0, sl - 62));
+            // lane L of O holds the bottom value of column s1-126+L: lanes 64-U..63 publish this
+            // body's U columns, then lane 63 the progress word (LDS is in order per wave)
+            const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
+            if (top - consKnown > kRing - 2 * U)
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    consKnown = uniform(*consOut);
+                    if (top - consKnown <= kRing - 2 * U) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+                }
+            }
+            const int col = s1 - 126 + lane;
+            if (lane >= kWave - U && col >= 1 && col <= n && col > published) rout[(col - 1) & kRingMask] = O;
+            if (lane == kWave - 1 && top > published) *progOut = top;
+            published = top;
         }
         if constexpr (LOCAL)
         {
@@ -364,34 +404,42 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
                 sfor<R>([&](auto Rc) {
                     constexpr int rho = decltype(Rc)::value;
                     const int key = best[rho];
-                    const int H = key >> kb;
+                    const int Hv = key >> kb;
                     const int st = blockBase + (kmask - (key & kmask));
-                    const int col = st - lane + 1;
+                    const int c = st - lane + 1;
                     const int row = rowTop + rho;
-                    if (H > 0 && row <= m && col >= 1 && col <= n)
+                    if (Hv > 0 && row <= m && c >= 1 && c <= n)
                     {
-                        const uint64_t k64 = ((uint64_t)H << (2 * kKeyRowBits)) |
+                        const uint64_t k64 = ((uint64_t)Hv << (2 * kKeyRowBits)) |
                                              ((kKeyMask - (uint64_t)row) << kKeyRowBits) |
-                                             (kKeyMask - (uint64_t)col);
+                                             (kKeyMask - (uint64_t)c);
                         lbest = max(lbest, k64);
                     }
                     best[rho] = 0;
                 });
             }
         }
-        if (hasPrev && s1 < nSteps)
-        {
-            ok = uniform(wait_feed<U>(a, bin, s1, n, lane, gn)) != 0;
-            FB = (int)(uint32_t)gn;
-        }
-        sfor<U>([&](auto Qc) {
-            constexpr int q = decltype(Qc)::value;
-            T[q] = Tn[q];
-        });
+        return s1 >= nSteps || feed(s1);
+    };
+    for (int s0 = 0; ok && s0 < nSteps; s0 += 2 * U)
+    {
+        ok = body(s0, TA, TB);
+        if (ok) ok = body(s0 + U, TB, TA);
     }
 #ifndef SA_VECTOR_MASK_STORE
     sstore_flush();
 #endif
+    if (hasNext && lane == kWave - 1) *progOut = n;  // never leave the consumer waiting (abort)
+    if (a.timeline && lane == 0)
+    {
+        uint64_t *tl = a.timeline + 4 * (size_t)idx;
+        tl[0] = tStart;
+        tl[1] = tFed;
+        tl[2] = __builtin_amdgcn_s_memrealtime();
+        // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
+        tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    }
     if constexpr (LOCAL)
     {
         const uint64_t wbest = wave_max_u64(lbest);
@@ -412,28 +460,128 @@ __device__ void process_strip(const FillArgs &a, const int *__restrict__ ldsS, i
     }
 }
 
-template <int R, bool LOCAL, bool PACKED>
-__global__ __launch_bounds__(64) void fill_kernel(FillArgs a)
+// The I/O wave of a group: global granules of the previous group's last strip -> ring[0], and
+// ring[W'] (W' = compute waves with a strip) -> granules for the next group. Only lane 0 polls the
+// granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
+// load the fabric the running strips use); the bytes move 64 columns per instruction.
+__device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
 {
-    __shared__ int ldsS[32 * 32];
-    const int lane = threadIdx.x;
-    if constexpr (!PACKED)
+    const int first = grp * W;
+    const int last = min(first + W, a.num_strips) - 1;
+    const StripDesc sf = a.strips[first];
+    const StripDesc sl = a.strips[last];
+    const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
+    const int nOut = (sl.flags & kHasNext) ? (int)a.pairs[sl.pair].text_len : 0;
+    if (nIn == 0 && nOut == 0) return;
+    const int wl = last - first + 1;  // ring fed by the last strip
+    volatile lds_int *r0 = (volatile lds_int *)rings;
+    volatile lds_int *prog0 = (volatile lds_int *)&H.prog[0];
+    volatile lds_int *cons0 = (volatile lds_int *)&H.cons[0];
+    volatile lds_int *rl = (volatile lds_int *)(rings + wl * kRing);
+    volatile lds_int *progL = (volatile lds_int *)&H.prog[wl];
+    volatile lds_int *consL = (volatile lds_int *)&H.cons[wl];
+    const uint64_t *bin = a.bnd + sf.bnd_in;
+    uint64_t *bout = a.bnd + sl.bnd_out;
+    int copied = 0, drained = 0;
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
     {
-        for (int e = lane; e < a.A * a.A; e += kWave) ldsS[e] = a.score_tab[e];
-        __syncthreads();
-    }
-    while (true)
-    {
-        int idx = 0;
-        if (lane == 0) idx = (int)atomicAdd(&a.ctrl->queue_head, 1u);
-        idx = __builtin_amdgcn_readlane(idx, 0);
-        if (idx >= a.num_strips) break;
-        if (uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) break;
-        process_strip<R, LOCAL, PACKED>(a, ldsS, idx, lane);
+        bool moved = false;
+        if (copied < nIn)
+        {
+            const int room = uniform(*cons0) + kRing - copied;  // free ring slots
+            const int want = min(min(kWave, nIn - copied), room);
+            if (want >= min(16, nIn - copied))
+            {
+                uint64_t probe = 0;
+                if (lane == 0) probe = load_granule(bin + copied + min(want, 16) - 1);
+                if ((uint32_t)uniform((int)(uint32_t)(probe >> 32)) == a.epoch)
+                {
+                    const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
+                    const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
+                    const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
+                    if (lane < cnt) r0[(copied + lane) & kRingMask] = (int)(uint32_t)v;
+                    copied += cnt;
+                    if (lane == 0) *prog0 = copied;
+                    moved = cnt > 0;
+                }
+            }
+        }
+        if (drained < nOut)
+        {
+            const int avail = uniform(*progL);
+            const int upto = min(avail, drained + kWave);
+            if (upto - drained >= 16 || (avail >= nOut && upto > drained))
+            {
+                const int c = drained + lane;
+                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)rl[c & kRingMask]);
+                drained = upto;
+                if (lane == 0) *consL = drained;
+                moved = true;
+            }
+        }
+        if (moved)
+        {
+            t0 = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
+        {
+            // release both sides so the group drains (the launch reports the abort)
+            if (lane == 0)
+            {
+                *prog0 = nIn;
+                *consL = nOut + kRing;
+            }
+            return;
+        }
     }
 }
 
-__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int8_t *codes, int A, int scale)
+// One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
+// dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
+// predecessor has always been handed out before it: progress is guaranteed whatever the residency.
+template <int R, bool LOCAL, bool PACKED>
+__global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs a)
+{
+    extern __shared__ int lds_dyn[];
+    GroupHdr &H = *reinterpret_cast<GroupHdr *>(lds_dyn);
+    lds_int *rings = (lds_int *)(lds_dyn + sizeof(GroupHdr) / 4);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = uniform((int)(threadIdx.x / kWave));
+    const int W = (int)(blockDim.x / kWave) - 1;  // compute waves; wave W is the I/O wave
+    if constexpr (!PACKED)
+        for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
+    while (true)
+    {
+        __syncthreads();  // every wave is done with the previous group's rings
+        if (threadIdx.x == 0)
+        {
+            const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
+        }
+        if (threadIdx.x <= kMaxWaves)
+        {
+            H.prog[threadIdx.x] = 0;
+            H.cons[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        const int grp = uniform(H.group);
+        if (grp >= a.num_groups) break;
+        if (w == W)
+        {
+            io_wave(a, H, rings, grp, W, lane);
+        }
+        else
+        {
+            const int idx = grp * W + w;
+            if (idx < a.num_strips) process_strip<R, LOCAL, PACKED>(a, H, rings, idx, w, lane);
+        }
+    }
+}
+
+__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int scale)
 {
     const PairDesc pd = pairs[blockIdx.y];
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
@@ -441,7 +589,7 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
     {
         int c = text[pd.text_off + x];
         c = min(max(c, 0), A - 1);
-        codes[pd.code_off + kPad + x] = (int8_t)(c * scale);
+        codes[pd.code_off + kPad + x] = c * scale;
     }
 }
 
@@ -717,7 +865,7 @@ int dmalloc(T **p, size_t bytes)
 
 struct sa_plan {
     int device = 0;
-    int mode = 0, A = 0, gap = 0, R = 0, U = 0, key_bits = 12;
+    int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12;
     bool packed = false;
     int num_cu = 0;
     std::vector<PairDesc> pairs;
@@ -729,7 +877,7 @@ struct sa_plan {
     PairDesc *d_pairs = nullptr;
     StripDesc *d_strips = nullptr;
     int32_t *d_prof = nullptr, *d_table = nullptr;
-    int8_t *d_codes = nullptr;
+    int32_t *d_codes = nullptr;
     uint32_t *d_masks = nullptr;
     uint64_t *d_bnd = nullptr, *d_best = nullptr;
     int32_t *d_score = nullptr;
@@ -762,37 +910,51 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
     return mmax > 16384 ? 2 : 1;
 }
 
-template <int R, bool LOCAL, bool PACKED>
-void launch_fill_t(const FillArgs &a, int grid, hipStream_t st)
+// Waves per workgroup (strips per group). Chains of strips (pairs taller than one strip) hand
+// their rows off through LDS inside a group; single-strip pairs gain nothing from grouping.
+int choose_W(const std::vector<PairDesc> &pairs)
 {
-    hipLaunchKernelGGL((fill_kernel<R, LOCAL, PACKED>), dim3(grid), dim3(kWave), 0, st, a);
+    if (const char *e = std::getenv("SA_WAVES_PER_GROUP"))
+    {
+        const int w = std::atoi(e);
+        if (w >= 1 && w <= kMaxWaves) return w;
+    }
+    for (const PairDesc &d : pairs)
+        if (d.num_strips > 1) return 4;
+    return 1;
+}
+
+template <int R, bool LOCAL, bool PACKED>
+void launch_fill_t(const FillArgs &a, int grid, int W, hipStream_t st)
+{
+    hipLaunchKernelGGL((fill_kernel<R, LOCAL, PACKED>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
 }
 
 template <int R>
-void launch_fill_r(const FillArgs &a, bool local, bool packed, int grid, hipStream_t st)
+void launch_fill_r(const FillArgs &a, bool local, bool packed, int grid, int W, hipStream_t st)
 {
     if (local)
     {
-        if (packed) launch_fill_t<R, true, true>(a, grid, st);
-        else launch_fill_t<R, true, false>(a, grid, st);
+        if (packed) launch_fill_t<R, true, true>(a, grid, W, st);
+        else launch_fill_t<R, true, false>(a, grid, W, st);
     }
     else
     {
-        if (packed) launch_fill_t<R, false, true>(a, grid, st);
-        else launch_fill_t<R, false, false>(a, grid, st);
+        if (packed) launch_fill_t<R, false, true>(a, grid, W, st);
+        else launch_fill_t<R, false, false>(a, grid, W, st);
     }
 }
 
-void launch_fill(int R, const FillArgs &a, bool local, bool packed, int grid, hipStream_t st)
+void launch_fill(int R, const FillArgs &a, bool local, bool packed, int grid, int W, hipStream_t st)
 {
     switch (R)
     {
-    case 1: launch_fill_r<1>(a, local, packed, grid, st); break;
-    case 2: launch_fill_r<2>(a, local, packed, grid, st); break;
-    case 4: launch_fill_r<4>(a, local, packed, grid, st); break;
-    case 8: launch_fill_r<8>(a, local, packed, grid, st); break;
-    case 16: launch_fill_r<16>(a, local, packed, grid, st); break;
-    default: launch_fill_r<32>(a, local, packed, grid, st); break;
+    case 1: launch_fill_r<1>(a, local, packed, grid, W, st); break;
+    case 2: launch_fill_r<2>(a, local, packed, grid, W, st); break;
+    case 4: launch_fill_r<4>(a, local, packed, grid, W, st); break;
+    case 8: launch_fill_r<8>(a, local, packed, grid, W, st); break;
+    case 16: launch_fill_r<16>(a, local, packed, grid, W, st); break;
+    default: launch_fill_r<32>(a, local, packed, grid, W, st); break;
     }
 }
 
@@ -922,7 +1084,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         const uint64_t n = d.text_len, m = d.pattern_len;
         const int ns = (n == 0 || m == 0) ? 0 : (int)((m + RB - 1) / RB);
         d.num_strips = ns;
-        const int nsteps = (int)(((n + kWave - 1) + U - 1) / U * U);
+        const int nsteps = (int)(((n + kWave - 1) + 2 * U - 1) / (2 * U) * (2 * U));  // two bodies per loop trip
         for (int b = 0; b < ns; ++b)
         {
             StripDesc s;
@@ -941,6 +1103,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     if (pl->strips.size() >= (1u << 31)) { delete pl; restore(); return fail(SA_ERR_UNSUPPORTED, "too many strips"); }
     pl->out_bytes = outb;
     pl->bytes_masks = mask_entries * 16;
+    pl->W = choose_W(pl->pairs);
 
     // ---- tables ----
     std::vector<int32_t> prof(4, 0), table(A * A);
@@ -962,7 +1125,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     alloc(&pl->d_strips, sizeof(StripDesc) * std::max<size_t>(1, pl->strips.size()));
     alloc(&pl->d_prof, sizeof(int32_t) * 4);
     alloc(&pl->d_table, sizeof(int32_t) * A * A);
-    alloc(&pl->d_codes, code_bytes + 16);
+    alloc(&pl->d_codes, 4 * code_bytes + 16);
     alloc(&pl->d_masks, pl->bytes_masks + 16);
     alloc(&pl->d_bnd, granules * 8 + 16);
     alloc(&pl->d_best, sizeof(uint64_t) * std::max<size_t>(1, pl->strips.size()));
@@ -978,7 +1141,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
                hipMemcpy(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size(), hipMemcpyHostToDevice) == hipSuccess &&
                hipMemcpy(pl->d_prof, prof.data(), sizeof(int32_t) * 4, hipMemcpyHostToDevice) == hipSuccess &&
                hipMemcpy(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice) == hipSuccess &&
-               hipMemset(pl->d_codes, 0, code_bytes + 16) == hipSuccess &&
+               hipMemset(pl->d_codes, 0, 4 * code_bytes + 16) == hipSuccess &&
                hipMemset(pl->d_bnd, 0, granules * 8 + 16) == hipSuccess &&
                hipMemset(pl->d_best, 0, sizeof(uint64_t) * std::max<size_t>(1, pl->strips.size())) == hipSuccess;
     if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
@@ -1046,9 +1209,27 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const double secs = e ? std::atof(e) : 20.0;
             a.timeout_ticks = (uint64_t)(secs * 1e8);
         }
-        const int grid = std::min(ns, std::max(1, pl->num_cu) * 8);
-        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->packed, grid, st);
+        // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
+        const char *tlPath = std::getenv("SA_TIMELINE");
+        a.timeline = nullptr;
+        if (tlPath) HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * 4 * ns));
+        const int W = pl->W;
+        a.num_groups = (ns + W - 1) / W;
+        const int grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
+        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->packed, grid, W, st);
         HIP_TRY(hipGetLastError());
+        if (tlPath)
+        {
+            std::vector<uint64_t> tl(4 * (size_t)ns);
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMemcpy(tl.data(), a.timeline, tl.size() * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(hipFree(a.timeline));
+            if (FILE *f = std::fopen(tlPath, "wb"))
+            {
+                std::fwrite(tl.data(), 8, tl.size(), f);
+                std::fclose(f);
+            }
+        }
         if (int rc = debug_sync(st, "fill_kernel")) return rc;
     }
     pl->filled = true;

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Per-strip fill timeline (GPU, debug): runs one fill with SA_TIMELINE set and reports, for a
+chain of strips, the hand-off lag (start of strip k's first body minus that of strip k-1), the
+per-step time and where the strips ran (XCC / CU). Timestamps are s_memrealtime (100 MHz)."""
+import argparse
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=32768)
+    ap.add_argument("--m", type=int, default=32768)
+    ap.add_argument("--R", type=int, default=1)
+    ap.add_argument("--mode", type=int, default=0)
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--pairs", type=int, default=1, help="independent copies of the pair (contention test)")
+    args = ap.parse_args()
+    if args.waves:
+        os.environ["SA_WAVES_PER_GROUP"] = str(args.waves)
+    from sa_amd import synthetic
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    t = synthetic.random_sequence(6, args.n, 4)
+    p = synthetic.random_sequence(7, args.m, 4)
+    b = DeviceBatch(args.mode, S, 5, [t] * args.pairs, [p] * args.pairs, rows_per_lane=args.R)
+    b.fill()
+    b.fill()
+    path = os.path.join(tempfile.mkdtemp(), "tl.bin")
+    os.environ["SA_TIMELINE"] = path
+    b.fill()
+    del os.environ["SA_TIMELINE"]
+    import torch
+    torch.cuda.synchronize()
+    tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
+    start, fed, end = (tl[:, i].astype(np.int64) for i in range(3))
+    xcc = (tl[:, 3] >> 32).astype(np.int64)
+    hw = (tl[:, 3] & 0xffffffff).astype(np.int64)
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    t0 = start.min()
+    nsteps = args.n + 63
+    lag = np.diff(fed) * 10.0 if len(fed) > 1 else np.zeros(1)  # ns
+    step_ns = (end - fed) * 10.0 / nsteps
+    W = int(os.environ.get("SA_WAVES_PER_GROUP", "4"))
+    k = np.arange(1, len(fed))
+    cross = (k % W) == 0
+    rec = {
+        "n": args.n, "m": args.m, "R": args.R, "W": W, "pairs": args.pairs, "strips": len(fed),
+        "total_us": round((end.max() - t0) * 0.01, 2),
+        "first_fed_us": round((fed[0] - t0) * 0.01, 3),
+        "last_start_us": round((start[-1] - t0) * 0.01, 2),
+        "ns_per_step_mean": round(float(step_ns.mean()), 2),
+        "ns_per_step_min": round(float(step_ns.min()), 2),
+        "ns_per_step_max": round(float(step_ns.max()), 2),
+        "lag_ns_in_group_mean": round(float(lag[~cross].mean()), 1) if (~cross).any() else None,
+        "lag_ns_cross_group_mean": round(float(lag[cross].mean()), 1) if cross.any() else None,
+        "lag_ns_p50": round(float(np.percentile(lag, 50)), 1),
+        "lag_ns_p90": round(float(np.percentile(lag, 90)), 1),
+        "lag_ns_max": round(float(lag.max()), 1),
+        "start_wait_ns_mean": round(float(((fed - start) * 10.0).mean()), 1),
+        "ns_per_step_by_strip": [round(float(x), 1) for x in step_ns[:: max(1, len(step_ns) // 16)]],
+        "lag_ns_by_strip": [round(float(x), 1) for x in lag[:: max(1, len(lag) // 16)]],
+        "xcc_of_first_16": xcc[:16].tolist(),
+        "cu_se_of_first_8": [(int(c), int(s)) for c, s in zip(cu[:8], se[:8])],
+    }
+    print(json.dumps(rec))
+    b.close()
+
+
+if __name__ == "__main__":
+    main()
