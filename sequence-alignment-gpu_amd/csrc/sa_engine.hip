@@ -68,14 +68,19 @@ __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
 
 // Direction planes go to memory straight from the SGPRs the ballots produced: one scalar-pipe
 // s_store_dwordx4 per (step,row) slot = {plane0, plane1} (no VALU work). The scalar data cache is
-// written back with s_dcache_wb at the end of every strip. SA_VECTOR_MASK_STORE selects the
-// alternative (v_writelane into a VGPR per 16 slots + one coalesced global store).
+// written back with s_dcache_wb at the end of every strip. The s_nop keeps the next instruction
+// from overwriting the store's data SGPRs before the store has read them (SA_SSTORE_NO_NOP drops
+// it, for measurement).
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <int OFF>
 __device__ __forceinline__ void sstore_slot(uint32_t *base, uint64_t p0, uint64_t p1)
 {
     const u32x4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
+#ifdef SA_SSTORE_NO_NOP
+    asm volatile("s_store_dwordx4 %0, %1, %2" ::"s"(v), "s"(base), "i"(OFF) : "memory");
+#else
     asm volatile("s_store_dwordx4 %0, %1, %2\n\ts_nop 0" ::"s"(v), "s"(base), "i"(OFF) : "memory");
+#endif
 }
 __device__ __forceinline__ void sstore_flush()
 {
@@ -149,6 +154,7 @@ struct FillArgs {
     int32_t key_bits;
     uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
     uint64_t *timeline;         // debug (SA_TIMELINE): per strip {start, fed, end, hw id}, or null
+    int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
 };
 
 // Work unit of the fill kernel: a GROUP of W consecutive strips. A workgroup has W compute waves
@@ -159,6 +165,12 @@ struct FillArgs {
 // the compute waves matters: on gfx9 a store shares the vmcnt counter with the text-code loads, and
 // a cross-XCD (sc1) store takes ~0.7 us to retire, which would stall the next load wait.
 typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, never flat
+// Ring and progress-word accesses are relaxed workgroup-scope atomics: the compiler keeps them in
+// program order and re-reads them every time, without the s_waitcnt lgkmcnt(0) it puts after every
+// volatile access (that wait would also drain the wave's outstanding scalar direction stores).
+// LDS executes one wave's ds operations in order, which is the only ordering the rings rely on.
+__device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 constexpr int kRing = 2048;        // ring entries (columns), power of two
 constexpr int kRingMask = kRing - 1;
 constexpr int kMaxWaves = 8;       // compute waves per workgroup
@@ -184,45 +196,67 @@ __device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int
 }
 
 // Waits until the producer wave has published columns 1..need into the ring (LDS progress word).
-__device__ __forceinline__ bool wait_ring(const FillArgs &a, volatile lds_int *prog, int need, int &avail, int lane)
+__device__ __forceinline__ bool wait_ring(const FillArgs &a, lds_int *prog, int need, int &avail, int lane)
 {
     if (avail >= need) return true;
-    avail = uniform(*prog);
+    avail = uniform(lds_ld(prog));
     if (avail >= need) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spin = 1;; ++spin)
     {
         __builtin_amdgcn_s_sleep(1);
-        avail = uniform(*prog);
+        avail = uniform(lds_ld(prog));
         if (avail >= need) return true;
         if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
     }
 }
 
-// One unrolled body of U steps. RAMP: some lanes are outside [1,n] and must keep their state.
-template <int R, bool LOCAL, bool PACKED, bool RAMP>
+// One unrolled body of U steps. Body kinds (KIND):
+//   kSteady  every lane is on a column >= 1. Lanes past column n compute garbage, which is harmless:
+//            it only ever flows to lanes that are past n as well, their direction planes are never
+//            read, their bottom-row values are never published and their local best-cell keys are
+//            filtered by column; only the global score and the local best-cell keys need the exact
+//            final state (kGeneric).
+//   kStart   the first bodies (s < 63): lane k is still left of column 1 while s < k. Forcing the
+//            substitution score of those virtual cells to 0 keeps their state at the boundary
+//            value 0 (F = max(0+0, 0, 0); H = max(0+0, -g, -g, 0)), so lane k enters column 1 with
+//            exactly the column-0 state: one compare + one select per cell instead of masking all
+//            of the state.
+//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row).
+enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
+// Per step the wave needs two lane moves: the row above each lane's first row (lane k reads lane
+// k-1; lane 0 reads the strip above) and the strip's bottom row leaving lane 63. Both go through one
+// queue register Q: lanes 0..U-1 hold the U values lane 0 will need this body (column s+1 first),
+// and every step Q moves down one lane (wave_shl:1) while lane 63 takes the new bottom value. After
+// U steps lanes 64-U..63 hold this body's U bottom-row values, lanes 0..U-1 are reloaded.
+// Direction planes: plane0 = DIAG, plane1 = raw "up > left" (global; the decoder resolves
+// DIAG before TOP) or (TOP & ~DIAG) | STOP, plane0 = DIAG | STOP (local). A plane pair is stored
+// one slot late, so the scalar store never waits on the v_cmp that has just produced its SGPRs.
+template <int R, bool LOCAL, bool PACKED, int KIND>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
-                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &FB,
-                                         int &O, uint32_t (&acc)[Cfg<R>::NACC], uint32_t *mbase)
+                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &Q,
+                                         uint32_t *mbase)
 {
     constexpr int U = Cfg<R>::U;
+    uint64_t pend0 = 0, pend1 = 0;
     sfor<U>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
         const int s = s0 + q;
         const int t = T[q];
         // value of the row above this lane's first row, at this lane's column
-        int up = dpp_shr1(FB, F[R - 1]);
-        FB = dpp_rol1(FB);
+        int up = dpp_shr1(Q, F[R - 1]);
         int diag = upPrev;
         upPrev = up;
         int gu = up - g;  // local only
+        constexpr bool RAMP = KIND == kGeneric;
         bool act = true;
         if constexpr (RAMP)
         {
             const int c = s - lane;
             act = (c >= 0) && (c < n);
         }
+        const bool real = KIND != kStart || lane <= s;  // kStart: column s-lane+1 >= 1
         const int kmask = (1 << kb) - 1;
         const int Ks = kmask - (s & kmask);  // local: later column in a block = smaller key
         sfor<R>([&](auto Rc) {
@@ -230,6 +264,7 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
             int sc;
             if constexpr (PACKED) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
             else sc = ldsS[prof[rho] + t];
+            if constexpr (KIND == kStart) sc = real ? sc : 0;
             uint64_t p0, p1;
             if constexpr (!LOCAL)
             {
@@ -237,14 +272,12 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 const int D = diag + sc;
                 const int M = max(left, up);
                 int Fn = max(D, M);
-                const uint64_t d = ballot(D > M);
-                const uint64_t tp = ballot(up > left);
+                p0 = ballot(D > M);
+                p1 = ballot(up > left);
                 if constexpr (RAMP) Fn = act ? Fn : left;
                 diag = left;
                 up = Fn;
                 F[rho] = Fn;
-                p0 = d;
-                p1 = tp & ~d;
             }
             else
             {
@@ -276,27 +309,26 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 p1 = (tp & ~d) | z;
             }
             constexpr int slot = q * R + rho;
-#ifdef SA_VECTOR_MASK_STORE
-            constexpr int ai = slot / 16, l = (slot % 16) * 4;
-            writelane<l + 0>(acc[ai], (uint32_t)p0);
-            writelane<l + 1>(acc[ai], (uint32_t)(p0 >> 32));
-            writelane<l + 2>(acc[ai], (uint32_t)p1);
-            writelane<l + 3>(acc[ai], (uint32_t)(p1 >> 32));
-#else
-            (void)acc;
-            sstore_slot<slot * 16>(mbase, p0, p1);
-#endif
+            if constexpr (slot > 0)
+            {
+                // keep this slot's work above the previous slot's store (scheduling fences only)
+                __builtin_amdgcn_sched_barrier(0);
+                sstore_slot<(slot - 1) * 16>(mbase, pend0, pend1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            pend0 = p0;
+            pend1 = p1;
         });
-        // collect the strip's bottom row: lane 63 appends, everything else moves down one lane
-        O = dpp_shl1(F[R - 1], O);
+        // the queue moves down one lane; lane 63 takes the strip's new bottom-row value
+        Q = dpp_shl1(F[R - 1], Q);
     });
+    sstore_slot<(U * R - 1) * 16>(mbase, pend0, pend1);
 }
 
 template <int R, bool LOCAL, bool PACKED>
 __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
-    constexpr int NACC = Cfg<R>::NACC;
     const StripDesc sd = a.strips[idx];
     const PairDesc pd = a.pairs[sd.pair];
     const int n = (int)pd.text_len, m = (int)pd.pattern_len;
@@ -314,14 +346,19 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
     const int32_t *codes = a.codes + pd.code_off + kPad;
     const bool hasPrev = (sd.flags & kHasPrev) != 0;
     const bool hasNext = (sd.flags & kHasNext) != 0;
-    volatile lds_int *rin = (volatile lds_int *)(rings + w * kRing);
-    volatile lds_int *rout = (volatile lds_int *)(rings + (w + 1) * kRing);
-    volatile lds_int *progIn = (volatile lds_int *)&H.prog[w];
-    volatile lds_int *consIn = (volatile lds_int *)&H.cons[w];
-    volatile lds_int *progOut = (volatile lds_int *)&H.prog[w + 1];
-    volatile lds_int *consOut = (volatile lds_int *)&H.cons[w + 1];
+    lds_int *rin = (lds_int *)(rings + w * kRing);
+    lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
+    lds_int *progIn = (lds_int *)&H.prog[w];
+    lds_int *consIn = (lds_int *)&H.cons[w];
+    lds_int *progOut = (lds_int *)&H.prog[w + 1];
+    lds_int *consOut = (lds_int *)&H.cons[w + 1];
     uint32_t *mk = a.masks + sd.mask_off * 4;
     const int nSteps = sd.nsteps;  // a multiple of 2U
+    // Lanes must stop at column n (kGeneric bodies at the end) where the final state is read: the
+    // global score H(m, n) in the strip holding row m, and the local best-cell keys (a garbage key
+    // past column n could shadow a real one of the same key block). Other strips run their tail
+    // unmasked.
+    const bool needFinal = LOCAL || (m - sd.row0 >= 0 && m - sd.row0 < kWave * R);
 
     // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
     int F[R], G[R], best[R];
@@ -331,7 +368,7 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
         G[rho] = -g;
         best[rho] = 0;
     });
-    int upPrev = 0, FB = 0, O = 0;
+    int upPrev = 0, Q = 0;
     // text codes, double-buffered across the two bodies of one loop trip (no register copies);
     // lane k at step s needs the code of column s-k+1, i.e. codes[s - k]
     int TA[U], TB[U];
@@ -351,32 +388,50 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
     bool ok = true;
     int avail = 0;       // columns known to be in rin
     int consKnown = 0;   // columns the consumer of rout is known to have read
-    // lanes 0..U-1 take the bottom values of columns base+1 .. base+U of the strip above
-    auto feed = [&](int base) -> bool {
-        if (!hasPrev) return true;  // row 0 boundary: FB stays 0
-        if (!wait_ring(a, progIn, min(n, base + U), avail, lane)) return false;
-        FB = (lane < U && base + lane < n) ? rin[(base + lane) & kRingMask] : 0;
-        if (lane == 0) *consIn = base + U;
+    // lanes 0..U-1 take the bottom values of columns base+1 .. base+U of the strip above. The
+    // progress word and the values are read speculatively one body ahead (LDS is in order: values
+    // read after a progress word that covers them are valid), so a feed that is already there
+    // costs no LDS round trip at the body boundary.
+    int pfProg = 0, pfVal = 0;
+    auto prefetch_feed = [&](int base) {
+        if (!hasPrev) return;
+        pfProg = lds_ld(progIn);
+        pfVal = lds_ld(rin + ((base + lane) & kRingMask));
+    };
+    auto feed = [&](int base) -> bool {  // (hasPrev only)
+        const int need = min(n, base + U);
+        if (uniform(pfProg) >= need)
+        {
+            avail = uniform(pfProg);
+        }
+        else
+        {
+            if (!wait_ring(a, progIn, need, avail, lane)) return false;
+            pfVal = lds_ld(rin + ((base + lane) & kRingMask));
+        }
+        Q = base + lane < n ? pfVal : 0;  // lanes >= U: don't care
+        if (lane == 0) lds_st(consIn, base + U);
         return true;
     };
-    ok = feed(0);
+    prefetch_feed(0);
+    if (hasPrev) ok = feed(0);
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     int published = 0;
     uint64_t lbest = 0;
     auto body = [&](int s0, int (&T)[U], int (&Tn)[U]) -> bool {
         const int s1 = s0 + U;
         load_codes(s1, Tn);  // prefetch one body ahead
-        uint32_t acc[NACC];
-        sfor<NACC>([&](auto Cc) { acc[decltype(Cc)::value] = 0; });
+        if (s1 < nSteps) prefetch_feed(s1);
         uint32_t *mbase = uniform_ptr(mk + (size_t)s0 * R * 4);  // this body's first direction entry
-        const bool steady = (s0 >= kWave - 1) && (s1 <= n);
-        if (steady)
-            run_body<R, LOCAL, PACKED, false>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
+        if (needFinal && s1 > n)
+            run_body<R, LOCAL, PACKED, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
+        else if (s0 < kWave - 1)
+            run_body<R, LOCAL, PACKED, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
         else
-            run_body<R, LOCAL, PACKED, true>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, FB, O, acc, mbase);
+            run_body<R, LOCAL, PACKED, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
         if (hasNext)
         {
-            // lane L of O holds the bottom value of column s1-126+L: lanes 64-U..63 publish this
+            // lane L of Q holds the bottom value of column s1-126+L: lanes 64-U..63 publish this
             // body's U columns, then lane 63 the progress word (LDS is in order per wave)
             const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
             if (top - consKnown > kRing - 2 * U)
@@ -384,15 +439,15 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
                 const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
                 for (uint32_t spin = 1;; ++spin)
                 {
-                    consKnown = uniform(*consOut);
+                    consKnown = uniform(lds_ld(consOut));
                     if (top - consKnown <= kRing - 2 * U) break;
                     __builtin_amdgcn_s_sleep(1);
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
                 }
             }
             const int col = s1 - 126 + lane;
-            if (lane >= kWave - U && col >= 1 && col <= n && col > published) rout[(col - 1) & kRingMask] = O;
-            if (lane == kWave - 1 && top > published) *progOut = top;
+            if (lane >= kWave - U && col >= 1 && col <= n && col > published) lds_st(rout + ((col - 1) & kRingMask), Q);
+            if (lane == kWave - 1 && top > published) lds_st(progOut, top);
             published = top;
         }
         if constexpr (LOCAL)
@@ -419,17 +474,21 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
                 });
             }
         }
-        return s1 >= nSteps || feed(s1);
+        if (s1 >= nSteps) return true;
+        if (!hasPrev)
+        {
+            Q = 0;  // row 0 boundary
+            return true;
+        }
+        return feed(s1);
     };
     for (int s0 = 0; ok && s0 < nSteps; s0 += 2 * U)
     {
         ok = body(s0, TA, TB);
         if (ok) ok = body(s0 + U, TB, TA);
     }
-#ifndef SA_VECTOR_MASK_STORE
     sstore_flush();
-#endif
-    if (hasNext && lane == kWave - 1) *progOut = n;  // never leave the consumer waiting (abort)
+    if (hasNext && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
     if (a.timeline && lane == 0)
     {
         uint64_t *tl = a.timeline + 4 * (size_t)idx;
@@ -474,12 +533,12 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
     const int nOut = (sl.flags & kHasNext) ? (int)a.pairs[sl.pair].text_len : 0;
     if (nIn == 0 && nOut == 0) return;
     const int wl = last - first + 1;  // ring fed by the last strip
-    volatile lds_int *r0 = (volatile lds_int *)rings;
-    volatile lds_int *prog0 = (volatile lds_int *)&H.prog[0];
-    volatile lds_int *cons0 = (volatile lds_int *)&H.cons[0];
-    volatile lds_int *rl = (volatile lds_int *)(rings + wl * kRing);
-    volatile lds_int *progL = (volatile lds_int *)&H.prog[wl];
-    volatile lds_int *consL = (volatile lds_int *)&H.cons[wl];
+    lds_int *r0 = (lds_int *)rings;
+    lds_int *prog0 = (lds_int *)&H.prog[0];
+    lds_int *cons0 = (lds_int *)&H.cons[0];
+    lds_int *rl = (lds_int *)(rings + wl * kRing);
+    lds_int *progL = (lds_int *)&H.prog[wl];
+    lds_int *consL = (lds_int *)&H.cons[wl];
     const uint64_t *bin = a.bnd + sf.bnd_in;
     uint64_t *bout = a.bnd + sl.bnd_out;
     int copied = 0, drained = 0;
@@ -489,7 +548,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
         bool moved = false;
         if (copied < nIn)
         {
-            const int room = uniform(*cons0) + kRing - copied;  // free ring slots
+            const int room = uniform(lds_ld(cons0)) + kRing - copied;  // free ring slots
             const int want = min(min(kWave, nIn - copied), room);
             if (want >= min(16, nIn - copied))
             {
@@ -500,23 +559,23 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
                     const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
                     const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
                     const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
-                    if (lane < cnt) r0[(copied + lane) & kRingMask] = (int)(uint32_t)v;
+                    if (lane < cnt) lds_st(r0 + ((copied + lane) & kRingMask), (int)(uint32_t)v);
                     copied += cnt;
-                    if (lane == 0) *prog0 = copied;
+                    if (lane == 0) lds_st(prog0, copied);
                     moved = cnt > 0;
                 }
             }
         }
         if (drained < nOut)
         {
-            const int avail = uniform(*progL);
+            const int avail = uniform(lds_ld(progL));
             const int upto = min(avail, drained + kWave);
             if (upto - drained >= 16 || (avail >= nOut && upto > drained))
             {
                 const int c = drained + lane;
-                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)rl[c & kRingMask]);
+                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)lds_ld(rl + (c & kRingMask)));
                 drained = upto;
-                if (lane == 0) *consL = drained;
+                if (lane == 0) lds_st(consL, drained);
                 moved = true;
             }
         }
@@ -525,14 +584,14 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
             t0 = __builtin_amdgcn_s_memrealtime();
             continue;
         }
-        __builtin_amdgcn_s_sleep(2);
+        for (int z = 0; z < a.io_sleep; ++z) __builtin_amdgcn_s_sleep(1);
         if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
         {
             // release both sides so the group drains (the launch reports the abort)
             if (lane == 0)
             {
-                *prog0 = nIn;
-                *consL = nOut + kRing;
+                lds_st(prog0, nIn);
+                lds_st(consL, nOut + kRing);
             }
             return;
         }
@@ -679,7 +738,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         const uint4 e = win[(s - wlo) * R + rho];
         const uint32_t w0 = k < 32 ? e.x : e.y;
         const uint32_t w1 = k < 32 ? e.z : e.w;
-        return (int)((w0 >> (k & 31)) & 1u) | (int)(((w1 >> (k & 31)) & 1u) << 1);
+        const int b0 = (int)((w0 >> (k & 31)) & 1u), b1 = (int)((w1 >> (k & 31)) & 1u);
+        // global: plane1 is the raw "up > left" bit, DIAG wins; local: {DIAG|STOP, TOP&~DIAG|STOP}
+        return a.mode == SA_GLOBAL ? (b0 ? kDiag : (b1 ? kTop : kLeft)) : (b0 | (b1 << 1));
     };
 
     uint8_t *ops = a.ops + pd.out_off;
@@ -1209,6 +1270,10 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const double secs = e ? std::atof(e) : 20.0;
             a.timeout_ticks = (uint64_t)(secs * 1e8);
         }
+        {
+            const char *e = std::getenv("SA_IO_SLEEP");
+            a.io_sleep = e ? std::max(0, std::atoi(e)) : 4;
+        }
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = std::getenv("SA_TIMELINE");
         a.timeline = nullptr;
@@ -1339,7 +1404,8 @@ int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *strea
             const uint32_t *w = &h[e * 4];
             const uint32_t b0 = (w[k < 32 ? 0 : 1] >> (k & 31)) & 1u;
             const uint32_t b1 = (w[k < 32 ? 2 : 3] >> (k & 31)) & 1u;
-            M[i * cols + j] = (uint8_t)(b0 | (b1 << 1));
+            // global: plane1 is the raw "up > left" bit and DIAG wins (see run_body)
+            M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
         }
     }
     return SA_OK;

@@ -7,17 +7,20 @@
 // wavefront). A strip therefore takes n + 63 steps.
 //
 // DIRECTIONS. At every (step s, row-slot rho) the wave produces, for its 64 cells, two 64-bit
-// planes from wave ballots: bit k of plane0/plane1 is bit 0/1 of the reference DIRECTION code
-// (LEFT=0, DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) of lane k's cell. They are stored
-// as one 16-byte entry {plane0, plane1}; entry (s, rho) of strip b lives at
-//     masks[strip.mask_off + s*R + rho].
+// planes from wave ballots, stored as one 16-byte entry {plane0, plane1}; entry (s, rho) of strip
+// b lives at  masks[strip.mask_off + s*R + rho].  Bit k belongs to lane k's cell. The reference
+// DIRECTION code (LEFT=0, DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) is
+//   global: plane0 = DIAG, plane1 = "up > left";  code = plane0 ? DIAG : plane1 ? TOP : LEFT
+//   local:  plane0 = DIAG|STOP, plane1 = (TOP&~DIAG)|STOP;  code = plane0 | plane1 << 1
 // That is 2 bits per cell written to HBM (the reference writes 1 byte per cell,
 // alignSequenceGPU.cu:142); the algorithmic figure used for the roofline stays 1 B/cell.
 //
-// STRIP HAND-OFF. A strip's bottom row feeds the next strip's first row. It travels through a
-// granule array in global memory: granule c-1 holds {tag = epoch, value} of column c as one
-// 8-byte write-through store, so the consumer needs no flag and no fence (a tag match means the
-// value is there); the per-call epoch makes stale granules from earlier calls unreadable.
+// STRIP HAND-OFF. A strip's bottom row feeds the next strip's first row. Strips are processed in
+// groups of W consecutive strips by one workgroup (W compute waves + 1 I/O wave): inside a group
+// the row travels through an LDS ring, between groups through a granule array in global memory:
+// granule c-1 holds {tag = epoch, value} of column c as one 8-byte write-through store, so the
+// consumer needs no flag and no fence (a tag match means the value is there); the per-call epoch
+// makes stale granules from earlier calls unreadable.
 #pragma once
 #include <stdint.h>
 

@@ -56,6 +56,7 @@ __global__ __launch_bounds__(64) void step_kernel(const int8_t *codes8, const in
     long long t0 = clock64();
     int T[U], Tn[U], X[U];
     uint64_t P0[3], P1[3];
+    int pfp = 0, pfv = 0;
     constexpr bool LEAN = V >= 3;
     constexpr bool DW = V >= 5;
     (void)P0; (void)P1;
@@ -144,6 +145,23 @@ __global__ __launch_bounds__(64) void step_kernel(const int8_t *codes8, const in
             const int pv = __builtin_amdgcn_readfirstlane(R[2048 + 100]);
             if (pv == 12345) F += 1;
         }
+        if constexpr (V == 13 || V == 15)
+        {
+            // producer: lanes 48..63 publish 16 columns, lane 63 the progress word
+            typedef __attribute__((address_space(3))) int li;
+            if (lane >= 48) __hip_atomic_store((li *)(ring + ((s0 + lane) & 2047)), O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 63) __hip_atomic_store((li *)(ring + 2048 + 100), s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (V == 14 || V == 15)
+        {
+            typedef __attribute__((address_space(3))) int li;
+            const int pv = __builtin_amdgcn_readfirstlane(pfp);
+            if (pv == 12345) F += 1;
+            FB = lane < 16 ? pfv : FB;
+            pfp = __hip_atomic_load((li *)(ring + 2048 + 101), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            pfv = __hip_atomic_load((li *)(ring + ((s0 + lane) & 2047)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (lane == 0) __hip_atomic_store((li *)(ring + 2048 + 102), s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
         if constexpr (V == 11)
         {
             if (lane >= 48) __hip_atomic_store((uint64_t *)(masks + 64) + (s0 & 1023) + lane, (uint64_t)F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -195,7 +213,7 @@ int main(int argc, char **argv)
     hipMalloc(&mk, (size_t)maxb * nsteps * 16 + 64);
     hipMalloc(&out, maxb * 64 * 4);
     hipMalloc(&cyc, maxb * 8);
-    for (int blocks : {1, 512})
+    for (int blocks : {1})
     {
         run<0>(blocks, nsteps, c8, c32, mk, out, cyc);
         run<1>(blocks, nsteps, c8, c32, mk, out, cyc);
@@ -210,6 +228,9 @@ int main(int argc, char **argv)
         run<10>(blocks, nsteps, c8, c32, mk, out, cyc);
         run<11>(blocks, nsteps, c8, c32, mk, out, cyc);
         run<12>(blocks, nsteps, c8, c32, mk, out, cyc);
+        run<13>(blocks, nsteps, c8, c32, mk, out, cyc);
+        run<14>(blocks, nsteps, c8, c32, mk, out, cyc);
+        run<15>(blocks, nsteps, c8, c32, mk, out, cyc);
     }
     return 0;
 }
