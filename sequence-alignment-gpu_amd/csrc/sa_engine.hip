@@ -71,6 +71,12 @@ __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
 // written back with s_dcache_wb at the end of every strip. The s_nop keeps the next instruction
 // from overwriting the store's data SGPRs before the store has read them (SA_SSTORE_NO_NOP drops
 // it, for measurement).
+#ifndef SA_STORE_LATE
+#define SA_STORE_LATE 1   // store a slot's planes one slot later (off the v_cmp -> s_store stall)
+#endif
+#ifndef SA_STORE_FENCE
+#define SA_STORE_FENCE 0  // pin that order with scheduling barriers
+#endif
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 template <int OFF>
 __device__ __forceinline__ void sstore_slot(uint32_t *base, uint64_t p0, uint64_t p1)
@@ -173,7 +179,7 @@ __device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, 
 __device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 constexpr int kRing = 2048;        // ring entries (columns), power of two
 constexpr int kRingMask = kRing - 1;
-constexpr int kMaxWaves = 8;       // compute waves per workgroup
+constexpr int kMaxWaves = 4;       // compute waves per workgroup (+1 I/O wave: 320 threads, <= 256 VGPRs)
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
@@ -309,24 +315,37 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 p1 = (tp & ~d) | z;
             }
             constexpr int slot = q * R + rho;
+#if SA_STORE_LATE
             if constexpr (slot > 0)
             {
+#if SA_STORE_FENCE
                 // keep this slot's work above the previous slot's store (scheduling fences only)
                 __builtin_amdgcn_sched_barrier(0);
+#endif
                 sstore_slot<(slot - 1) * 16>(mbase, pend0, pend1);
+#if SA_STORE_FENCE
                 __builtin_amdgcn_sched_barrier(0);
+#endif
             }
             pend0 = p0;
             pend1 = p1;
+#else
+            sstore_slot<slot * 16>(mbase, p0, p1);
+#endif
         });
         // the queue moves down one lane; lane 63 takes the strip's new bottom-row value
         Q = dpp_shl1(F[R - 1], Q);
     });
+#if SA_STORE_LATE
     sstore_slot<(U * R - 1) * 16>(mbase, pend0, pend1);
+#else
+    (void)pend0;
+    (void)pend1;
+#endif
 }
 
 template <int R, bool LOCAL, bool PACKED>
-__device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
+__device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
     const StripDesc sd = a.strips[idx];
@@ -372,7 +391,7 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
     // text codes, double-buffered across the two bodies of one loop trip (no register copies);
     // lane k at step s needs the code of column s-k+1, i.e. codes[s - k]
     int TA[U], TB[U];
-    auto load_codes = [&](int s0, int (&dst)[U]) {
+    auto load_codes = [&](int s0, int (&dst)[U]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
         sfor<U / 4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value * 4;
@@ -393,12 +412,14 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
     // read after a progress word that covers them are valid), so a feed that is already there
     // costs no LDS round trip at the body boundary.
     int pfProg = 0, pfVal = 0;
-    auto prefetch_feed = [&](int base) {
+    auto prefetch_feed = [&](int base) __attribute__((always_inline)) {
         if (!hasPrev) return;
         pfProg = lds_ld(progIn);
+#ifndef SA_EXP_NO_FEED_READ
         pfVal = lds_ld(rin + ((base + lane) & kRingMask));
+#endif
     };
-    auto feed = [&](int base) -> bool {  // (hasPrev only)
+    auto feed = [&](int base) __attribute__((always_inline)) -> bool {  // (hasPrev only)
         const int need = min(n, base + U);
         if (uniform(pfProg) >= need)
         {
@@ -418,7 +439,7 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     int published = 0;
     uint64_t lbest = 0;
-    auto body = [&](int s0, int (&T)[U], int (&Tn)[U]) -> bool {
+    auto body = [&](int s0, int (&T)[U], int (&Tn)[U]) __attribute__((always_inline)) -> bool {
         const int s1 = s0 + U;
         load_codes(s1, Tn);  // prefetch one body ahead
         if (s1 < nSteps) prefetch_feed(s1);
@@ -446,7 +467,9 @@ __device__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, in
                 }
             }
             const int col = s1 - 126 + lane;
+#ifndef SA_EXP_NO_PUBLISH
             if (lane >= kWave - U && col >= 1 && col <= n && col > published) lds_st(rout + ((col - 1) & kRingMask), Q);
+#endif
             if (lane == kWave - 1 && top > published) lds_st(progOut, top);
             published = top;
         }
@@ -655,7 +678,9 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
 // ------------------------------------------------------------------------------------------------
 // traceback kernel
 // ------------------------------------------------------------------------------------------------
-constexpr int kWinEntries = 2048;  // 32 KiB LDS window of 16-byte direction entries
+constexpr int kWinEntries = 1024;  // entries (16 bytes each) per LDS window buffer: 2 x 16 KiB
+constexpr int kWinPerLane = kWinEntries / 64;
+constexpr int kNearTop = 8;        // rows below a strip's top at which the next strip is prefetched
 
 struct TbArgs {
     const int8_t *text, *pattern;
@@ -676,11 +701,10 @@ enum { kLeft = 0, kDiag = 1, kTop = 2, kStop = 3 };  // SequenceAlignment.hpp:12
 template <int R>
 __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
 {
-    __shared__ uint4 win[kWinEntries];
+    __shared__ uint4 win[2][kWinEntries];
     __shared__ char alpha[40];
     __shared__ int scan[2][kWave];
     constexpr int RB = kWave * R;
-    constexpr int WSTEPS = kWinEntries / R;
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     const PairDesc pd = a.pairs[p];
@@ -714,60 +738,127 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         }
     }
 
-    int wb = -1, wlo = 0, whi = -1;
-    auto code_at = [&](int ci, int cj) -> int {
-        const int b = (ci - 1) / RB;
-        const int il = (ci - 1) - b * RB;
-        const int k = il / R, rho = il % R;
-        const int s = cj - 1 + k;
-        if (b != wb || s < wlo || s > whi)
+    // ---- the walk: a uniform state machine (scalar registers) --------------------------------
+    // Row i lives in strip b at in-strip row il = (i-1) - b*RB, i.e. lane k = il/R, slot il%R; the
+    // entry of cell (i, j) is e = (j-1+k)*R + il%R of strip b. A move changes e by a constant:
+    //   TOP  -1 (also across a lane boundary),  LEFT -R,  DIAG -R-1,
+    // and il by -1 for TOP/DIAG; only leaving the strip (il < 0) re-derives e. Within a strip e only
+    // decreases, so the walk reads a strip's entries top-down through windows of kWinEntries entries
+    // held in LDS (one of two buffers). The next window is loaded ahead into registers (16 x 16 bytes
+    // per lane, in flight while the walk goes on): the one below in the same strip, or, once the walk
+    // is within kNearTop rows of the strip's top, the top window of the strip above. Each step reads
+    // just the two dwords that hold bit k of the two planes.
+    constexpr int LOG2R = R == 1 ? 0 : R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5;
+    // all strips of a pair have the same step count and consecutive entry ranges, so no strip
+    // descriptor is loaded inside the walk (such a load would drain the prefetch in flight: gfx9
+    // retires vector loads in order)
+    uint64_t maskOff0 = 0;
+    int stripEntries = 0;
+    if (pd.num_strips > 0)
+    {
+        const StripDesc s0d = a.strips[pd.first_strip];
+        maskOff0 = s0d.mask_off;
+        stripEntries = s0d.nsteps * R;
+    }
+    int b = 0, il = 0, e = 0;
+    auto enter = [&](int ii, int jj) __attribute__((always_inline)) {  // (i, j) -> b, il, e
+        b = (ii - 1) / RB;
+        il = (ii - 1) - b * RB;
+        e = (jj - 1 + (il >> LOG2R)) * R + (il & (R - 1));
+    };
+    u32x4 stage[kWinPerLane];  // native vectors: promoted to registers (HIP's uint4 struct is not)
+    int cur = 0, curStrip = -1, curLo = 0;
+    int pfStrip = -1, pfLo = 0;  // window held in `stage` (pfStrip -1: none)
+    auto stage_load = [&](int strip, int lo) __attribute__((always_inline)) {
+        const int last = stripEntries - 1;
+        const u32x4 *src = reinterpret_cast<const u32x4 *>(a.masks + maskOff0 + (uint64_t)strip * stripEntries);
+        sfor<kWinPerLane>([&](auto Tc) {
+            constexpr int t = decltype(Tc)::value;
+            stage[t] = src[min(lo + t * kWave + lane, last)];
+        });
+        pfStrip = strip;
+        pfLo = lo;
+    };
+    auto stage_commit = [&]() __attribute__((always_inline)) {  // staged window -> the other buffer
+        const int nb = cur ^ 1;
+        sfor<kWinPerLane>([&](auto Tc) {
+            constexpr int t = decltype(Tc)::value;
+            *reinterpret_cast<u32x4 *>(&win[nb][t * kWave + lane]) = stage[t];
+        });
+        cur = nb;
+        curStrip = pfStrip;
+        curLo = pfLo;
+        pfStrip = -1;
+    };
+    // make entry e of strip b readable; prefetch what comes next
+    auto ensure = [&](int jj) __attribute__((always_inline)) {
+        if (b != curStrip || e < curLo)
         {
-            __syncthreads();
-            wb = b;
-            whi = s;
-            wlo = max(0, s - WSTEPS + 1);
-            const StripDesc sd = a.strips[pd.first_strip + b];
-            const uint4 *src = a.masks + sd.mask_off + (uint64_t)wlo * R;
-            const int cnt = (whi - wlo + 1) * R;
-#ifdef SA_TB_DEBUG
-            if (lane == 0) printf("reload i=%d j=%d b=%d k=%d rho=%d s=%d wlo=%d whi=%d off=%llu cnt=%d nsteps=%d\n", ci, cj, b, k, rho, s, wlo, whi, (unsigned long long)sd.mask_off, cnt, sd.nsteps);
-#endif
-            for (int e = lane; e < cnt; e += kWave) win[e] = src[e];
-            __syncthreads();
+            if (!(b == pfStrip && e >= pfLo && e < pfLo + kWinEntries)) stage_load(b, max(0, e - kWinEntries + 1));
+            stage_commit();
+            if (curLo > 0) stage_load(b, max(0, curLo - kWinEntries));
         }
-        const uint4 e = win[(s - wlo) * R + rho];
-        const uint32_t w0 = k < 32 ? e.x : e.y;
-        const uint32_t w1 = k < 32 ? e.z : e.w;
+        if (il < kNearTop && b > 0 && pfStrip != b - 1)
+            stage_load(b - 1, max(0, (jj - 1 + kWave - 1) * R + R - 1 - kWinEntries + 1));
+    };
+    const uint32_t *winw = reinterpret_cast<const uint32_t *>(&win[0][0]);
+    auto code_at = [&](int jj) __attribute__((always_inline)) -> int {
+        ensure(jj);
+        const int k = il >> LOG2R;
+        const int dw = cur * (kWinEntries * 4) + (e - curLo) * 4 + (k >> 5);
+        const uint32_t w0 = (uint32_t)uniform((int)winw[dw]);
+        const uint32_t w1 = (uint32_t)uniform((int)winw[dw + 2]);
         const int b0 = (int)((w0 >> (k & 31)) & 1u), b1 = (int)((w1 >> (k & 31)) & 1u);
         // global: plane1 is the raw "up > left" bit, DIAG wins; local: {DIAG|STOP, TOP&~DIAG|STOP}
         return a.mode == SA_GLOBAL ? (b0 ? kDiag : (b1 ? kTop : kLeft)) : (b0 | (b1 << 1));
     };
+    auto move = [&](int tt, int tp, int ni, int nj) __attribute__((always_inline)) {  // after i -= tp, j -= tt
+        e -= (tt << LOG2R) + tp;
+        il -= tp;
+        if (il < 0 && ni > 0) enter(ni, nj);
+    };
 
+    // ops are collected 64 at a time in one VGPR (v_writelane at lane len%64), then stored by all
+    // lanes as 64 consecutive bytes
     uint8_t *ops = a.ops + pd.out_off;
+    int opsAcc = 0;
+    int len = 0;
+    auto emit = [&](int d) __attribute__((always_inline)) {
+        opsAcc = amdgcn_writelane(d, len & (kWave - 1), opsAcc);
+        ++len;
+        if ((len & (kWave - 1)) == 0) ops[len - kWave + lane] = (uint8_t)opsAcc;
+    };
     // text / pattern index of the first letter the walk emits (the start cell's)
     const int ti0 = a.mode == SA_GLOBAL ? n - 1 : j - 1;
     const int pi0 = a.mode == SA_GLOBAL ? m - 1 : i - 1;
-    int len = 0, ti, pi;
+    int ti, pi;
+    if (i > 0 && j > 0) enter(i, j);
     if (a.mode == SA_GLOBAL)
     {
         // traceBackNW (alignSequenceCPU.cpp:64-114): row 0 forces LEFT, column 0 forces TOP
         ti = n - 1;
         pi = m - 1;
-        while (i > 0 || j > 0)
+        while (i > 0 && j > 0)
         {
-            const int d = j == 0 ? kTop : (i == 0 ? kLeft : code_at(i, j));
-            const int tt = d == kDiag || d == kLeft;
-            const int tp = d == kDiag || d == kTop;
-#ifdef SA_TB_DEBUG
-            if (lane == 0 && len >= n + m) printf("BAD len=%d i=%d j=%d d=%d\n", len, i, j, d);
-            if (lane == 0 && len < 4000) printf("mv %d %d %d %d\n", len, i, j, d);
-#endif
-            if (lane == 0) ops[len] = (uint8_t)d;
-            ++len;
+            const int d = code_at(j);
+            const int tt = d != kTop;   // DIAG or LEFT
+            const int tp = d != kLeft;  // DIAG or TOP
+            emit(d);
             ti = max(0, ti - tt);
             pi = max(0, pi - tp);
             i -= tp;
             j -= tt;
+            move(tt, tp, i, j);
+        }
+        // the boundary: only TOP moves down column 0, only LEFT moves along row 0
+        while (i > 0 || j > 0)
+        {
+            const int tp = j == 0;
+            emit(tp ? kTop : kLeft);
+            ti = max(0, ti - (1 - tp));
+            pi = max(0, pi - tp);
+            i -= tp;
+            j -= 1 - tp;
         }
     }
     else
@@ -778,22 +869,22 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         pi = i - 1;
         while (i > 0 && j > 0)
         {
-            const int d = code_at(i, j);
+            const int d = code_at(j);
             if (d == kStop) break;
-            const int tt = d == kDiag || d == kLeft;
-            const int tp = d == kDiag || d == kTop;
-#ifdef SA_TB_DEBUG
-            if (lane == 0 && len >= n + m) printf("BAD len=%d i=%d j=%d d=%d\n", len, i, j, d);
-            if (lane == 0 && len < 4000) printf("mv %d %d %d %d\n", len, i, j, d);
-#endif
-            if (lane == 0) ops[len] = (uint8_t)d;
-            ++len;
+            const int tt = d != kTop;
+            const int tp = d != kLeft;
+            emit(d);
             i -= tp;
             j -= tt;
             if (i == 0 || j == 0) break;
-            ti = max(0, ti - tt);
-            pi = max(0, pi - tp);
+            ti -= tt;
+            pi -= tp;
+            move(tt, tp, i, j);
         }
+    }
+    {
+        const int rem = len & (kWave - 1);
+        if (lane < rem) ops[len - rem + lane] = (uint8_t)opsAcc;
     }
     if (lane == 0)
     {
@@ -962,13 +1053,16 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
     for (int64_t p = 0; p < np; ++p) mmax = std::max<uint64_t>(mmax, pairs[p].pattern_len);
     if (np >= 256)
     {
-        // many independent pairs: one strip per pair where possible (no hand-offs at all)
+        // many independent pairs: one strip per pair where possible (no hand-offs at all); local
+        // mode keeps 3 registers per row (H, G, best key) and stops at 16 rows per lane, where
+        // its working set still fits the register file
+        const int rmax = P->mode == SA_LOCAL ? 16 : 32;
         int r = 1;
-        while (r < 32 && (uint64_t)kWave * r < mmax) r <<= 1;
+        while (r < rmax && (uint64_t)kWave * r < mmax) r <<= 1;
         return r;
     }
-    // few long pairs: short strips keep the wavefront pipeline deep
-    return mmax > 16384 ? 2 : 1;
+    // few long pairs: the shortest strips keep the wavefront deepest (one row per lane)
+    return 1;
 }
 
 // Waves per workgroup (strips per group). Chains of strips (pairs taller than one strip) hand

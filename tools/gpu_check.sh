@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU box check used during development: parity tests, then the three bench workloads (no CPU
+# baseline) -> gpurun_out/<tag>_*.log. Every GPU step has its own time limit; stops at the first failure.
+tag=${1:-chk}
+timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/${tag}_tests.log 2>&1 || { tail -n 30 gpurun_out/${tag}_tests.log; exit 1; }
+tail -n 1 gpurun_out/${tag}_tests.log
+for w in headline local batch; do
+  timeout -k 10 300 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/${tag}_$w.log 2>&1 || { tail -n 20 gpurun_out/${tag}_$w.log; exit 1; }
+done
