@@ -78,9 +78,18 @@ __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
 #define SA_STORE_FENCE 0  // pin that order with scheduling barriers
 #endif
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#ifdef SA_EXP_NO_DIRSTORE
+__device__ uint64_t g_exp_sink;
+#endif
 template <int OFF>
 __device__ __forceinline__ void sstore_slot(uint32_t *base, uint64_t p0, uint64_t p1)
 {
+#ifdef SA_EXP_NO_DIRSTORE
+    // timing experiment only: keep the ballots alive without storing them
+    asm volatile("" ::"s"(p0), "s"(p1));
+    (void)base;
+    return;
+#endif
     const u32x4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
 #ifdef SA_SSTORE_NO_NOP
     asm volatile("s_store_dwordx4 %0, %1, %2" ::"s"(v), "s"(base), "i"(OFF) : "memory");
@@ -678,7 +687,7 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
 // ------------------------------------------------------------------------------------------------
 // traceback kernel
 // ------------------------------------------------------------------------------------------------
-constexpr int kWinEntries = 1024;  // entries (16 bytes each) per LDS window buffer: 2 x 16 KiB
+constexpr int kWinEntries = 512;   // entries (16 bytes each) per LDS window buffer: 2 x 8 KiB
 constexpr int kWinPerLane = kWinEntries / 64;
 constexpr int kNearTop = 8;        // rows below a strip's top at which the next strip is prefetched
 
