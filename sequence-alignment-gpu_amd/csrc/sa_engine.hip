@@ -8,18 +8,19 @@
 //   local best cell (first max)       :191-192
 //   tracebacks                        traceBackNW :64-114, traceBackSW :10-62
 //
-// Fill kernel (one wave64 per strip, dynamic strip queue):
+// Fill kernel (one wave64 per strip; workgroups of W strips + an I/O wave; dynamic group queue):
 //   * lane k owns R rows and works on column s-k+1 at step s; the value from the row above
-//     arrives by a DPP wave_shr:1 lane shift, lane 0 is fed from the strip above (granules);
+//     arrives by a DPP wave_shr:1 lane shift, lane 0 is fed from the strip above through an LDS
+//     ring (inside a workgroup) or epoch-tagged global granules moved by the I/O wave;
 //   * the substitution score comes from a per-row profile register (DNA: four int8 scores packed
 //     in one VGPR, selected by v_bfe_i32 on the text code) or from an LDS table (protein);
 //   * global alignment runs in the shifted domain F = H + g*(i+j), where the recurrence
 //     becomes F = max(Fdiag + s + 2g, Fleft, Fup) and every boundary is 0;
 //   * the direction of each cell is never materialised per lane: two wave ballots per
-//     (step,row) are the two bit-planes of the DIRECTION code, collected with v_writelane into
-//     one VGPR per 16 (step,row) slots and written as coalesced 256-byte stores.
-// Traceback kernel (one wave per pair): walks the bit-planes through an LDS window, then
-// converts the op string to letters in parallel.
+//     (step,row) are the two bit-planes of the DIRECTION code, written with one scalar
+//     s_store_dwordx4 straight from the ballot SGPRs.
+// Traceback kernel (one wave per pair): a scalar walk over the bit-planes through double-buffered
+// LDS windows, then a parallel pass that converts the op string to letters.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
