@@ -16,9 +16,9 @@
 //     in one VGPR, selected by v_bfe_i32 on the text code) or from an LDS table (protein);
 //   * global alignment runs in the shifted domain F = H + g*(i+j), where the recurrence
 //     becomes F = max(Fdiag + s + 2g, Fleft, Fup) and every boundary is 0;
-//   * the direction of each cell is never materialised per lane: two wave ballots per
-//     (step,row) are the two bit-planes of the DIRECTION code, written with one scalar
-//     s_store_dwordx4 straight from the ballot SGPRs.
+//   * the direction of each cell is two bits pushed into per-lane VGPR words (one subtraction and
+//     one v_alignbit per bit, no SGPR round trip); every 32 (step,row) slots a lane's words go to
+//     HBM in one coalesced vector store per wave.
 // Traceback kernel (one wave per pair): a scalar walk over the bit-planes through double-buffered
 // LDS windows, then a parallel pass that converts the op string to letters.
 #include <hip/hip_runtime.h>
@@ -67,42 +67,18 @@ __device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
     acc = (uint32_t)amdgcn_writelane((int)v, L, (int)acc);
 }
 
-// Direction planes go to memory straight from the SGPRs the ballots produced: one scalar-pipe
-// s_store_dwordx4 per (step,row) slot = {plane0, plane1} (no VALU work). The scalar data cache is
-// written back with s_dcache_wb at the end of every strip. The s_nop keeps the next instruction
-// from overwriting the store's data SGPRs before the store has read them (SA_SSTORE_NO_NOP drops
-// it, for measurement).
-#ifndef SA_STORE_LATE
-#define SA_STORE_LATE 1   // store a slot's planes one slot later (off the v_cmp -> s_store stall)
-#endif
-#ifndef SA_STORE_FENCE
-#define SA_STORE_FENCE 0  // pin that order with scheduling barriers
-#endif
+// Direction bits are accumulated per lane, in VGPRs: push_sign shifts a word left by one and moves
+// the sign bit of x in (v_alignbit_b32 {acc, x} >> 31), so "a > b" costs one subtraction and one
+// alignbit, with no SGPR round trip. After 32 pushes a word holds 32 consecutive (step,row) slots of
+// one plane, most recent in bit 0; a chunk of words goes to HBM as one coalesced vector store per
+// lane (sa_layout.h). All values are bounded well inside int32, so the differences
+// never overflow.
+__device__ __forceinline__ uint32_t push_sign(uint32_t acc, int x)
+{
+    return __builtin_amdgcn_alignbit(acc, (uint32_t)x, 31);
+}
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-#ifdef SA_EXP_NO_DIRSTORE
-__device__ uint64_t g_exp_sink;
-#endif
-template <int OFF>
-__device__ __forceinline__ void sstore_slot(uint32_t *base, uint64_t p0, uint64_t p1)
-{
-#ifdef SA_EXP_NO_DIRSTORE
-    // timing experiment only: keep the ballots alive without storing them
-    asm volatile("" ::"s"(p0), "s"(p1));
-    (void)base;
-    return;
-#endif
-    const u32x4 v = {(uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32)};
-#ifdef SA_SSTORE_NO_NOP
-    asm volatile("s_store_dwordx4 %0, %1, %2" ::"s"(v), "s"(base), "i"(OFF) : "memory");
-#else
-    asm volatile("s_store_dwordx4 %0, %1, %2\n\ts_nop 0" ::"s"(v), "s"(base), "i"(OFF) : "memory");
-#endif
-}
-__device__ __forceinline__ void sstore_flush()
-{
-    __builtin_amdgcn_s_dcache_wb();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
@@ -145,9 +121,12 @@ __device__ __forceinline__ void store_granule(uint64_t *p, uint64_t v)
 template <int R>
 struct Cfg {
     static constexpr int U = (16 / R) > 4 ? (16 / R) : 4;  // steps per unrolled body
-    static constexpr int SLOTS = U * R;                     // (step,row) slots per body
-    static constexpr int NACC = SLOTS / 16;                 // direction accumulators (VGPRs)
-    static_assert(SLOTS % 16 == 0, "body must fill whole accumulators");
+    static constexpr int SB = U * R;                        // (step,row) slots per body
+    static constexpr int CS = SB > 32 ? SB : 32;            // slots per stored chunk (sa_layout.h)
+    static constexpr int NW = CS / 32;                      // words per plane per lane per chunk
+    static constexpr int LW = 2 * NW;                       // dwords per lane per chunk (2 planes)
+    static constexpr int BPC = CS / SB;                     // bodies per chunk (1 or 2)
+    static_assert(SB % 16 == 0 && (CS % SB) == 0, "bodies must tile chunks");
 };
 
 struct FillArgs {
@@ -183,7 +162,7 @@ struct FillArgs {
 typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, never flat
 // Ring and progress-word accesses are relaxed workgroup-scope atomics: the compiler keeps them in
 // program order and re-reads them every time, without the s_waitcnt lgkmcnt(0) it puts after every
-// volatile access (that wait would also drain the wave's outstanding scalar direction stores).
+// volatile access.
 // LDS executes one wave's ds operations in order, which is the only ordering the rings rely on.
 __device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -245,17 +224,18 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // queue register Q: lanes 0..U-1 hold the U values lane 0 will need this body (column s+1 first),
 // and every step Q moves down one lane (wave_shl:1) while lane 63 takes the new bottom value. After
 // U steps lanes 64-U..63 hold this body's U bottom-row values, lanes 0..U-1 are reloaded.
-// Direction planes: plane0 = DIAG, plane1 = raw "up > left" (global; the decoder resolves
-// DIAG before TOP) or (TOP & ~DIAG) | STOP, plane0 = DIAG | STOP (local). A plane pair is stored
-// one slot late, so the scalar store never waits on the v_cmp that has just produced its SGPRs.
+// Direction bits (pushed per lane, see push_sign): global pushes D > M into plane 0 and the raw
+// "up > left" into plane 1 (the decoder lets DIAG win); local pushes D > M, gu > Gl and H == 0 into
+// three words that the chunk store folds into plane 0 = DIAG | STOP, plane 1 = (TOP & ~DIAG) | STOP.
+// Slot (q, rho) of this body is slot SB*bodyInChunk + q*R + rho of the chunk, i.e. word
+// (q*R + rho) / 32 when a body fills whole words (SB >= 32); otherwise every push goes to word 0.
 template <int R, bool LOCAL, bool PACKED, int KIND>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
                                          int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &Q,
-                                         uint32_t *mbase)
+                                         uint32_t (&acc)[3][Cfg<R>::NW])
 {
     constexpr int U = Cfg<R>::U;
-    uint64_t pend0 = 0, pend1 = 0;
     sfor<U>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
         const int s = s0 + q;
@@ -277,19 +257,19 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
         const int Ks = kmask - (s & kmask);  // local: later column in a block = smaller key
         sfor<R>([&](auto Rc) {
             constexpr int rho = decltype(Rc)::value;
+            constexpr int w = ((q * R + rho) / 32) % Cfg<R>::NW;
             int sc;
             if constexpr (PACKED) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
             else sc = ldsS[prof[rho] + t];
             if constexpr (KIND == kStart) sc = real ? sc : 0;
-            uint64_t p0, p1;
             if constexpr (!LOCAL)
             {
                 const int left = F[rho];
                 const int D = diag + sc;
                 const int M = max(left, up);
                 int Fn = max(D, M);
-                p0 = ballot(D > M);
-                p1 = ballot(up > left);
+                acc[0][w] = push_sign(acc[0][w], M - D);     // DIAG
+                acc[1][w] = push_sign(acc[1][w], left - up); // up > left
                 if constexpr (RAMP) Fn = act ? Fn : left;
                 diag = left;
                 up = Fn;
@@ -301,9 +281,9 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 const int D = diag + sc;
                 const int M = max(Gl, gu);
                 int Hn = max(max(D, M), 0);
-                const uint64_t d = ballot(D > M);
-                const uint64_t tp = ballot(gu > Gl);
-                const uint64_t z = ballot(Hn == 0);
+                acc[0][w] = push_sign(acc[0][w], M - D);     // DIAG
+                acc[1][w] = push_sign(acc[1][w], Gl - gu);   // raw TOP
+                acc[2][w] = push_sign(acc[2][w], Hn - 1);    // STOP (H == 0)
                 int Gn = Hn - g;
                 const int key = (Hn << kb) + Ks;
                 if constexpr (RAMP)
@@ -321,37 +301,44 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 gu = Gn;
                 F[rho] = Hn;
                 G[rho] = Gn;
-                p0 = d | z;
-                p1 = (tp & ~d) | z;
             }
-            constexpr int slot = q * R + rho;
-#if SA_STORE_LATE
-            if constexpr (slot > 0)
-            {
-#if SA_STORE_FENCE
-                // keep this slot's work above the previous slot's store (scheduling fences only)
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-                sstore_slot<(slot - 1) * 16>(mbase, pend0, pend1);
-#if SA_STORE_FENCE
-                __builtin_amdgcn_sched_barrier(0);
-#endif
-            }
-            pend0 = p0;
-            pend1 = p1;
-#else
-            sstore_slot<slot * 16>(mbase, p0, p1);
-#endif
         });
         // the queue moves down one lane; lane 63 takes the strip's new bottom-row value
         Q = dpp_shl1(F[R - 1], Q);
     });
-#if SA_STORE_LATE
-    sstore_slot<(U * R - 1) * 16>(mbase, pend0, pend1);
-#else
-    (void)pend0;
-    (void)pend1;
-#endif
+}
+
+// Stores one finished chunk: lane k's LW dwords at chunk*64*LW + k*LW (one coalesced wave store).
+template <int R, bool LOCAL>
+__device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)[3][Cfg<R>::NW])
+{
+    constexpr int NW = Cfg<R>::NW;
+    uint32_t v[2 * NW];
+    sfor<NW>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        if constexpr (LOCAL)
+        {
+            const uint32_t d = acc[0][w], t = acc[1][w], z = acc[2][w];
+            v[w] = d | z;
+            v[NW + w] = (t & ~d) | z;
+        }
+        else
+        {
+            v[w] = acc[0][w];
+            v[NW + w] = acc[1][w];
+        }
+    });
+    if constexpr (NW == 1)
+    {
+        *reinterpret_cast<u32x2 *>(dst) = u32x2{v[0], v[1]};
+    }
+    else
+    {
+        sfor<NW / 2>([&](auto Xc) {
+            constexpr int x = decltype(Xc)::value;
+            *reinterpret_cast<u32x4 *>(dst + 4 * x) = u32x4{v[4 * x], v[4 * x + 1], v[4 * x + 2], v[4 * x + 3]};
+        });
+    }
 }
 
 template <int R, bool LOCAL, bool PACKED>
@@ -381,7 +368,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     lds_int *consIn = (lds_int *)&H.cons[w];
     lds_int *progOut = (lds_int *)&H.prog[w + 1];
     lds_int *consOut = (lds_int *)&H.cons[w + 1];
-    uint32_t *mk = a.masks + sd.mask_off * 4;
+    // this lane's first dword in the strip's direction chunks
+    uint32_t *mk = a.masks + sd.mask_off * 4 + lane * Cfg<R>::LW;
+    uint32_t acc[3][Cfg<R>::NW];
+    sfor<Cfg<R>::NW>([&](auto Wc) {
+        acc[0][decltype(Wc)::value] = 0;
+        acc[1][decltype(Wc)::value] = 0;
+        acc[2][decltype(Wc)::value] = 0;
+    });
     const int nSteps = sd.nsteps;  // a multiple of 2U
     // Lanes must stop at column n (kGeneric bodies at the end) where the final state is read: the
     // global score H(m, n) in the strip holding row m, and the local best-cell keys (a garbage key
@@ -453,13 +447,18 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         const int s1 = s0 + U;
         load_codes(s1, Tn);  // prefetch one body ahead
         if (s1 < nSteps) prefetch_feed(s1);
-        uint32_t *mbase = uniform_ptr(mk + (size_t)s0 * R * 4);  // this body's first direction entry
         if (needFinal && s1 > n)
-            run_body<R, LOCAL, PACKED, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
+            run_body<R, LOCAL, PACKED, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
         else if (s0 < kWave - 1)
-            run_body<R, LOCAL, PACKED, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
+            run_body<R, LOCAL, PACKED, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
         else
-            run_body<R, LOCAL, PACKED, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, mbase);
+            run_body<R, LOCAL, PACKED, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
+        // a chunk is complete after BPC bodies: s1*R slots done, a multiple of CS
+        if (Cfg<R>::BPC == 1 || ((s1 * R) & (Cfg<R>::CS - 1)) == 0)
+        {
+            const int chunk = (s1 * R) / Cfg<R>::CS - 1;
+            store_chunk<R, LOCAL>(mk + (size_t)chunk * (kWave * Cfg<R>::LW), acc);
+        }
         if (hasNext)
         {
             // lane L of Q holds the bottom value of column s1-126+L: lanes 64-U..63 publish this
@@ -520,7 +519,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         ok = body(s0, TA, TB);
         if (ok) ok = body(s0 + U, TB, TA);
     }
-    sstore_flush();
     if (hasNext && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
     if (a.timeline && lane == 0)
     {
@@ -759,6 +757,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
     // is within kNearTop rows of the strip's top, the top window of the strip above. Each step reads
     // just the two dwords that hold bit k of the two planes.
     constexpr int LOG2R = R == 1 ? 0 : R == 2 ? 1 : R == 4 ? 2 : R == 8 ? 3 : R == 16 ? 4 : 5;
+    constexpr int CS = Cfg<R>::CS, NW = Cfg<R>::NW, LW = Cfg<R>::LW;
+    constexpr int LOG2CS = CS == 32 ? 5 : CS == 64 ? 6 : 7;
+    static_assert((1 << LOG2CS) == CS && kWinEntries % CS == 0, "windows hold whole chunks");
     // all strips of a pair have the same step count and consecutive entry ranges, so no strip
     // descriptor is loaded inside the walk (such a load would drain the prefetch in flight: gfx9
     // retires vector loads in order)
@@ -804,21 +805,24 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
     auto ensure = [&](int jj) __attribute__((always_inline)) {
         if (b != curStrip || e < curLo)
         {
-            if (!(b == pfStrip && e >= pfLo && e < pfLo + kWinEntries)) stage_load(b, max(0, e - kWinEntries + 1));
+            if (!(b == pfStrip && e >= pfLo && e < pfLo + kWinEntries)) stage_load(b, e & ~(kWinEntries - 1));
             stage_commit();
-            if (curLo > 0) stage_load(b, max(0, curLo - kWinEntries));
+            if (curLo > 0) stage_load(b, curLo - kWinEntries);
         }
         if (il < kNearTop && b > 0 && pfStrip != b - 1)
-            stage_load(b - 1, max(0, (jj - 1 + kWave - 1) * R + R - 1 - kWinEntries + 1));
+            stage_load(b - 1, ((jj - 1 + kWave - 1) * R + R - 1) & ~(kWinEntries - 1));
     };
     const uint32_t *winw = reinterpret_cast<const uint32_t *>(&win[0][0]);
     auto code_at = [&](int jj) __attribute__((always_inline)) -> int {
         ensure(jj);
+        // slot rel of the window: chunk rel/CS, lane k's words, bit 31 - rel%32 (sa_layout.h)
         const int k = il >> LOG2R;
-        const int dw = cur * (kWinEntries * 4) + (e - curLo) * 4 + (k >> 5);
+        const int rel = e - curLo;
+        const int dw = cur * (kWinEntries * 4) + (rel >> LOG2CS) * (kWave * LW) + k * LW + ((rel & (CS - 1)) >> 5);
         const uint32_t w0 = (uint32_t)uniform((int)winw[dw]);
-        const uint32_t w1 = (uint32_t)uniform((int)winw[dw + 2]);
-        const int b0 = (int)((w0 >> (k & 31)) & 1u), b1 = (int)((w1 >> (k & 31)) & 1u);
+        const uint32_t w1 = (uint32_t)uniform((int)winw[dw + NW]);
+        const int sh = 31 - (rel & 31);
+        const int b0 = (int)((w0 >> sh) & 1u), b1 = (int)((w1 >> sh) & 1u);
         // global: plane1 is the raw "up > left" bit, DIAG wins; local: {DIAG|STOP, TOP&~DIAG|STOP}
         return a.mode == SA_GLOBAL ? (b0 ? kDiag : (b1 ? kTop : kLeft)) : (b0 | (b1 << 1));
     };
@@ -1498,16 +1502,18 @@ int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *strea
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipSetDevice(cur));
     const int R = pl->R, RB = kWave * R;
+    const uint64_t CS = std::max(32, pl->U * R), NW = CS / 32, LW = 2 * NW;  // Cfg<R>
     for (uint64_t i = 1; i <= m; ++i)
     {
         const uint64_t b = (i - 1) / RB, il = (i - 1) % RB, k = il / R, rho = il % R;
         const StripDesc &sd = pl->strips[pd.first_strip + b];
         for (uint64_t j = 1; j <= n; ++j)
         {
-            const uint64_t e = (sd.mask_off - e0) + (j - 1 + k) * R + rho;
-            const uint32_t *w = &h[e * 4];
-            const uint32_t b0 = (w[k < 32 ? 0 : 1] >> (k & 31)) & 1u;
-            const uint32_t b1 = (w[k < 32 ? 2 : 3] >> (k & 31)) & 1u;
+            // slot e of the strip: chunk e/CS, lane k's LW words, plane word (e%CS)/32, bit 31-e%32
+            const uint64_t e = (j - 1 + k) * R + rho;
+            const uint32_t *w = &h[(sd.mask_off - e0) * 4 + (e / CS) * kWave * LW + k * LW + (e % CS) / 32];
+            const uint32_t b0 = (w[0] >> (31 - e % 32)) & 1u;
+            const uint32_t b1 = (w[NW] >> (31 - e % 32)) & 1u;
             // global: plane1 is the raw "up > left" bit and DIAG wins (see run_body)
             M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
         }

@@ -6,10 +6,15 @@
 // working on column  j = s - k + 1  at step s (a one-column skew per lane, the anti-diagonal
 // wavefront). A strip therefore takes n + 63 steps.
 //
-// DIRECTIONS. At every (step s, row-slot rho) the wave produces, for its 64 cells, two 64-bit
-// planes from wave ballots, stored as one 16-byte entry {plane0, plane1}; entry (s, rho) of strip
-// b lives at  masks[strip.mask_off + s*R + rho].  Bit k belongs to lane k's cell. The reference
-// DIRECTION code (LEFT=0, DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) is
+// DIRECTIONS. Every (step s, row-slot rho) of a strip is a SLOT  e = s*R + rho  holding two bits
+// per lane (two planes). Lane k accumulates its own bits in VGPR words and the strip's slots are
+// stored in CHUNKS of CS = max(32, U*R) slots (U = steps per unrolled body): chunk c is
+// 64 lanes x LW dwords (LW = 2*CS/32), lane k's LW dwords contiguous = {plane0 words, plane1
+// words}, each word 32 consecutive slots with the first slot in bit 31. So slot e of lane k is bit
+// 31 - e%32 of dword  c*64*LW + k*LW + P*(CS/32) + (e%CS)/32  (c = e/CS, plane P) from the strip's
+// base  masks + 16*strip.mask_off  bytes. That is 16 bytes per slot, and a range of slots that
+// starts on a chunk boundary is a contiguous byte range. The reference DIRECTION code (LEFT=0,
+// DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) is
 //   global: plane0 = DIAG, plane1 = "up > left";  code = plane0 ? DIAG : plane1 ? TOP : LEFT
 //   local:  plane0 = DIAG|STOP, plane1 = (TOP&~DIAG)|STOP;  code = plane0 | plane1 << 1
 // That is 2 bits per cell written to HBM (the reference writes 1 byte per cell,
@@ -36,7 +41,7 @@ struct StripDesc {
     int32_t row0;       // first DP row (1-based) of the strip
     int32_t flags;      // kHasPrev | kHasNext
     int32_t nsteps;     // steps this strip runs (n + 63 rounded up to the body length)
-    uint64_t mask_off;  // first 16-byte direction entry
+    uint64_t mask_off;  // first direction slot (16 bytes per slot, see DIRECTIONS)
     uint64_t bnd_in;    // granule index of the predecessor's bottom row (kHasPrev)
     uint64_t bnd_out;   // granule index of this strip's bottom row (kHasNext)
 };
