@@ -206,6 +206,21 @@ __device__ __forceinline__ bool wait_ring(const FillArgs &a, lds_int *prog, int 
     }
 }
 
+// Ring slot of column c (1-based) in every LDS ring. The +14 puts the first column of a producer
+// body's bottom-row values (c = s0 - 62, s0 a multiple of U) on a slot that is a multiple of U, so
+// lane 63 publishes a body with U/4 ds_write_b128 that never straddle the ring's end.
+__device__ __forceinline__ int ring_slot(int c) { return (c + 14) & kRingMask; }
+static_assert(kRing % 16 == 0, "ring must hold whole bodies");
+
+// Where a strip's substitution scores come from (SK):
+//   kProf   DNA-sized alphabets: a per-row packed profile (four int8 scores in one VGPR) selected by
+//           v_bfe_i32 with the text code 8*c;
+//   kTable  other alphabets, R > 1: the A x A table in LDS indexed by row letter * A + text letter;
+//   kArr    R = 1: per-letter score arrays over the text ("text profiles": arr[a][x] = S[a][t[x]]
+//           (+2g global), zero padding on both sides), so the load delivers the score itself; the
+//           zero padding also keeps the ramp cells left of column 1 at the boundary value.
+enum ScoreKind { kProf = 0, kTable = 1, kArr = 2 };
+
 // One unrolled body of U steps. Body kinds (KIND):
 //   kSteady  every lane is on a column >= 1. Lanes past column n compute garbage, which is harmless:
 //            it only ever flows to lanes that are past n as well, their direction planes are never
@@ -216,32 +231,29 @@ __device__ __forceinline__ bool wait_ring(const FillArgs &a, lds_int *prog, int 
 //            substitution score of those virtual cells to 0 keeps their state at the boundary
 //            value 0 (F = max(0+0, 0, 0); H = max(0+0, -g, -g, 0)), so lane k enters column 1 with
 //            exactly the column-0 state: one compare + one select per cell instead of masking all
-//            of the state.
+//            of the state. (kArr strips need no kStart bodies: their padding scores are 0.)
 //   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row).
 enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
-// Per step the wave needs two lane moves: the row above each lane's first row (lane k reads lane
-// k-1; lane 0 reads the strip above) and the strip's bottom row leaving lane 63. Both go through one
-// queue register Q: lanes 0..U-1 hold the U values lane 0 will need this body (column s+1 first),
-// and every step Q moves down one lane (wave_shl:1) while lane 63 takes the new bottom value. After
-// U steps lanes 64-U..63 hold this body's U bottom-row values, lanes 0..U-1 are reloaded.
-// Direction bits (pushed per lane, see push_sign): global pushes D > M into plane 0 and the raw
-// "up > left" into plane 1 (the decoder lets DIAG win); local pushes D > M, gu > Gl and H == 0 into
-// three words that the chunk store folds into plane 0 = DIAG | STOP, plane 1 = (TOP & ~DIAG) | STOP.
-// Slot (q, rho) of this body is slot SB*bodyInChunk + q*R + rho of the chunk, i.e. word
-// (q*R + rho) / 32 when a body fills whole words (SB >= 32); otherwise every push goes to word 0.
-template <int R, bool LOCAL, bool PACKED, int KIND>
+// Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
+// wave_shr:1 whose `old` operand is this step's feed register Q (lane 0 keeps Q's lane 0 = the
+// strip above's bottom value for this column); Q is dead afterwards, so the DPP writes in place. The
+// next step's feed register is Q shifted down one lane (wave_shl:1, bound_ctrl), computed first.
+// The strip's bottom row (F[R-1] of lane 63 after each step) is not moved at all: every step's F[R-1]
+// stays in its own register Fs[q] until the body ends, when lane 63 publishes all U of them.
+template <int R, bool LOCAL, int SK, int KIND>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
-                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int &Q,
-                                         uint32_t (&acc)[3][Cfg<R>::NW])
+                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int Q,
+                                         int (&Fs)[Cfg<R>::U], uint32_t (&acc)[3][Cfg<R>::NW])
 {
     constexpr int U = Cfg<R>::U;
     sfor<U>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
         const int s = s0 + q;
         const int t = T[q];
-        // value of the row above this lane's first row, at this lane's column
+        const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
         int up = dpp_shr1(Q, F[R - 1]);
+        Q = Qn;
         int diag = upPrev;
         upPrev = up;
         int gu = up - g;  // local only
@@ -259,7 +271,8 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
             constexpr int rho = decltype(Rc)::value;
             constexpr int w = ((q * R + rho) / 32) % Cfg<R>::NW;
             int sc;
-            if constexpr (PACKED) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
+            if constexpr (SK == kArr) sc = t;
+            else if constexpr (SK == kProf) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
             else sc = ldsS[prof[rho] + t];
             if constexpr (KIND == kStart) sc = real ? sc : 0;
             if constexpr (!LOCAL)
@@ -303,8 +316,7 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 G[rho] = Gn;
             }
         });
-        // the queue moves down one lane; lane 63 takes the strip's new bottom-row value
-        Q = dpp_shl1(F[R - 1], Q);
+        Fs[q] = F[R - 1];
     });
 }
 
@@ -341,7 +353,7 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
     }
 }
 
-template <int R, bool LOCAL, bool PACKED>
+template <int R, bool LOCAL, int SK>
 __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
@@ -357,9 +369,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         const int i = rowTop + rho;
         int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
         c = min(max(c, 0), a.A - 1);
-        prof[rho] = PACKED ? a.prof_tab[c] : c * a.A;
+        prof[rho] = SK == kProf ? a.prof_tab[c] : SK == kTable ? c * a.A : c;
     });
-    const int32_t *codes = a.codes + pd.code_off + kPad;
+    // kArr: this lane's row letter selects its text profile (R = 1)
+    const int32_t *codes = a.codes + pd.code_off + (SK == kArr ? (uint64_t)prof[0] * pd.code_len : 0) + kPad;
     const bool hasPrev = (sd.flags & kHasPrev) != 0;
     const bool hasNext = (sd.flags & kHasNext) != 0;
     lds_int *rin = (lds_int *)(rings + w * kRing);
@@ -392,6 +405,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         best[rho] = 0;
     });
     int upPrev = 0, Q = 0;
+    int Fs[U];
     // text codes, double-buffered across the two bodies of one loop trip (no register copies);
     // lane k at step s needs the code of column s-k+1, i.e. codes[s - k]
     int TA[U], TB[U];
@@ -419,9 +433,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     auto prefetch_feed = [&](int base) __attribute__((always_inline)) {
         if (!hasPrev) return;
         pfProg = lds_ld(progIn);
-#ifndef SA_EXP_NO_FEED_READ
-        pfVal = lds_ld(rin + ((base + lane) & kRingMask));
-#endif
+        pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
     };
     auto feed = [&](int base) __attribute__((always_inline)) -> bool {  // (hasPrev only)
         const int need = min(n, base + U);
@@ -432,7 +444,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         else
         {
             if (!wait_ring(a, progIn, need, avail, lane)) return false;
-            pfVal = lds_ld(rin + ((base + lane) & kRingMask));
+            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
         }
         Q = base + lane < n ? pfVal : 0;  // lanes >= U: don't care
         if (lane == 0) lds_st(consIn, base + U);
@@ -448,11 +460,11 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         load_codes(s1, Tn);  // prefetch one body ahead
         if (s1 < nSteps) prefetch_feed(s1);
         if (needFinal && s1 > n)
-            run_body<R, LOCAL, PACKED, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
-        else if (s0 < kWave - 1)
-            run_body<R, LOCAL, PACKED, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
+            run_body<R, LOCAL, SK, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
+        else if (SK != kArr && s0 < kWave - 1)
+            run_body<R, LOCAL, SK, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
         else
-            run_body<R, LOCAL, PACKED, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, acc);
+            run_body<R, LOCAL, SK, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
         // a chunk is complete after BPC bodies: s1*R slots done, a multiple of CS
         if (Cfg<R>::BPC == 1 || ((s1 * R) & (Cfg<R>::CS - 1)) == 0)
         {
@@ -461,24 +473,39 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         }
         if (hasNext)
         {
-            // lane L of Q holds the bottom value of column s1-126+L: lanes 64-U..63 publish this
-            // body's U columns, then lane 63 the progress word (LDS is in order per wave)
+            // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
+            // columns <= 0 are ramp garbage that lands in ring slots of columns far ahead (never
+            // yet published), columns > n are never read
+            const int c0 = s0 - (kWave - 2);
             const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
-            if (top - consKnown > kRing - 2 * U)
+            if (c0 + U - 1 >= 1 && c0 <= n)
             {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                for (uint32_t spin = 1;; ++spin)
+                // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
+                if (c0 + U - 1 - kRing > consKnown)
                 {
-                    consKnown = uniform(lds_ld(consOut));
-                    if (top - consKnown <= kRing - 2 * U) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    for (uint32_t spin = 1;; ++spin)
+                    {
+                        consKnown = uniform(lds_ld(consOut));
+                        if (c0 + U - 1 - kRing <= consKnown) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+                    }
                 }
+                if (lane == kWave - 1)
+                {
+                    typedef int i32x4 __attribute__((ext_vector_type(4)));
+                    typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
+                    lds_i32x4 *dst = (lds_i32x4 *)(rout + ring_slot(c0));
+                    sfor<U / 4>([&](auto Xc) {
+                        constexpr int x = decltype(Xc)::value;
+                        dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
+                    });
+                }
+                // the values go before the progress word: a compiler-only fence (LDS executes one
+                // wave's operations in order)
+                asm volatile("" ::: "memory");
             }
-            const int col = s1 - 126 + lane;
-#ifndef SA_EXP_NO_PUBLISH
-            if (lane >= kWave - U && col >= 1 && col <= n && col > published) lds_st(rout + ((col - 1) & kRingMask), Q);
-#endif
             if (lane == kWave - 1 && top > published) lds_st(progOut, top);
             published = top;
         }
@@ -590,7 +617,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
                     const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
                     const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
                     const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
-                    if (lane < cnt) lds_st(r0 + ((copied + lane) & kRingMask), (int)(uint32_t)v);
+                    if (lane < cnt) lds_st(r0 + ring_slot(copied + lane + 1), (int)(uint32_t)v);
                     copied += cnt;
                     if (lane == 0) lds_st(prog0, copied);
                     moved = cnt > 0;
@@ -604,7 +631,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
             if (upto - drained >= 16 || (avail >= nOut && upto > drained))
             {
                 const int c = drained + lane;
-                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)lds_ld(rl + (c & kRingMask)));
+                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)lds_ld(rl + ring_slot(c + 1)));
                 drained = upto;
                 if (lane == 0) lds_st(consL, drained);
                 moved = true;
@@ -632,7 +659,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, bool PACKED>
+template <int R, bool LOCAL, int SK>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -641,7 +668,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
     const int lane = threadIdx.x & (kWave - 1);
     const int w = uniform((int)(threadIdx.x / kWave));
     const int W = (int)(blockDim.x / kWave) - 1;  // compute waves; wave W is the I/O wave
-    if constexpr (!PACKED)
+    if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
     while (true)
     {
@@ -666,12 +693,16 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         else
         {
             const int idx = grp * W + w;
-            if (idx < a.num_strips) process_strip<R, LOCAL, PACKED>(a, H, rings, idx, w, lane);
+            if (idx < a.num_strips) process_strip<R, LOCAL, SK>(a, H, rings, idx, w, lane);
         }
     }
 }
 
-__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int scale)
+// Text codes for the fill: one dword per letter, 8*c (packed profile bit offset) or c (LDS table
+// index). With text profiles (R = 1) the pair's block holds A arrays of code_len dwords instead,
+// array a = the scores S[a][t[x]] (+2g for global) of row letter a against every text letter.
+__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int scale,
+                                   const int32_t *table, int profiles)
 {
     const PairDesc pd = pairs[blockIdx.y];
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
@@ -679,7 +710,10 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
     {
         int c = text[pd.text_off + x];
         c = min(max(c, 0), A - 1);
-        codes[pd.code_off + kPad + x] = c * scale;
+        if (profiles)
+            for (int r = 0; r < A; ++r) codes[pd.code_off + (uint64_t)r * pd.code_len + kPad + x] = table[r * A + c];
+        else
+            codes[pd.code_off + kPad + x] = c * scale;
     }
 }
 
@@ -1093,24 +1127,32 @@ int choose_W(const std::vector<PairDesc> &pairs)
     return 1;
 }
 
-template <int R, bool LOCAL, bool PACKED>
+template <int R, bool LOCAL, int SK>
 void launch_fill_t(const FillArgs &a, int grid, int W, hipStream_t st)
 {
-    hipLaunchKernelGGL((fill_kernel<R, LOCAL, PACKED>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
+    hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
 }
 
+// R = 1 always uses text profiles (kArr); taller strips use the packed profile when the scores fit
+// (kProf) and the LDS table otherwise (kTable).
 template <int R>
 void launch_fill_r(const FillArgs &a, bool local, bool packed, int grid, int W, hipStream_t st)
 {
-    if (local)
+    if constexpr (R == 1)
     {
-        if (packed) launch_fill_t<R, true, true>(a, grid, W, st);
-        else launch_fill_t<R, true, false>(a, grid, W, st);
+        (void)packed;
+        if (local) launch_fill_t<1, true, kArr>(a, grid, W, st);
+        else launch_fill_t<1, false, kArr>(a, grid, W, st);
+    }
+    else if (local)
+    {
+        if (packed) launch_fill_t<R, true, kProf>(a, grid, W, st);
+        else launch_fill_t<R, true, kTable>(a, grid, W, st);
     }
     else
     {
-        if (packed) launch_fill_t<R, false, true>(a, grid, W, st);
-        else launch_fill_t<R, false, false>(a, grid, W, st);
+        if (packed) launch_fill_t<R, false, kProf>(a, grid, W, st);
+        else launch_fill_t<R, false, kTable>(a, grid, W, st);
     }
 }
 
@@ -1246,7 +1288,8 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         d.pattern_off = pairs[p].pattern_offset;
         d.pattern_len = pairs[p].pattern_len;
         d.code_off = code_bytes;
-        code_bytes += kPad + d.text_len + 4 * kPad;
+        d.code_len = kPad + d.text_len + 4 * kPad;
+        code_bytes += (R == 1 ? (uint64_t)A : 1) * d.code_len;  // R = 1: A text profiles
         d.out_off = outb;
         outb += d.text_len + d.pattern_len + 16;
         d.first_strip = (int32_t)pl->strips.size();
@@ -1348,7 +1391,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             // pairs beyond 65535 are handled by re-basing the pair pointer
             const int cnt = std::min(65535, np - y0);
             hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
-                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->packed ? 8 : 1);
+                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->packed ? 8 : 1, pl->d_table, pl->R == 1 ? 1 : 0);
         }
         HIP_TRY(hipGetLastError());
         if (int rc = debug_sync(st, "encode_text_kernel")) return rc;

@@ -49,7 +49,8 @@ enum : int32_t { kHasPrev = 1, kHasNext = 2 };
 
 struct PairDesc {
     uint64_t text_off, text_len, pattern_off, pattern_len;
-    uint64_t code_off;     // start of this pair's padded text-code block
+    uint64_t code_off;     // start of this pair's padded text-code block (R = 1: A text profiles)
+    uint64_t code_len;     // dwords per code array: kPad + text_len + 4*kPad
     uint64_t out_off;      // start of this pair's output region (capacity text_len+pattern_len)
     int32_t first_strip, num_strips;
 };
