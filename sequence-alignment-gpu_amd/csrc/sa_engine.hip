@@ -212,28 +212,60 @@ __device__ __forceinline__ bool wait_ring(const FillArgs &a, lds_int *prog, int 
 __device__ __forceinline__ int ring_slot(int c) { return (c + 14) & kRingMask; }
 static_assert(kRing % 16 == 0, "ring must hold whole bodies");
 
-// Where a strip's substitution scores come from (SK):
-//   kProf   DNA-sized alphabets: a per-row packed profile (four int8 scores in one VGPR) selected by
-//           v_bfe_i32 with the text code 8*c;
+// Where a strip's substitution scores come from (SK). Every table already holds S + 2g (global) or
+// S + g (local), the offsets the recurrences below fold in:
+//   kProf   DNA-sized alphabets, R > 1: a per-row packed profile (four int8 scores in one VGPR)
+//           selected by v_bfe_i32 with the text code 8*c;
 //   kTable  other alphabets, R > 1: the A x A table in LDS indexed by row letter * A + text letter;
-//   kArr    R = 1: per-letter score arrays over the text ("text profiles": arr[a][x] = S[a][t[x]]
-//           (+2g global), zero padding on both sides), so the load delivers the score itself; the
-//           zero padding also keeps the ramp cells left of column 1 at the boundary value.
-enum ScoreKind { kProf = 0, kTable = 1, kArr = 2 };
+//   kArr    R = 1: per-letter score arrays over the text ("text profiles": arr[a][x] = S[a][t[x]]),
+//           zero padded on both sides, so the load delivers the score itself;
+//   kArr8   R = 1 when the scores fit int8: the same profiles as bytes, four byte-shifted copies
+//           per letter so that every lane's 16-byte load is dword aligned (lane k reads copy k%4);
+//           one global_load_dwordx4 serves a whole 16-step body and the byte is picked by the
+//           add itself (SDWA src1_sel:BYTE_q, sign-extended).
+// The zero padding of the profiles keeps the ramp cells left of column 1 at the boundary value.
+enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3 };
+template <int SK>
+constexpr bool kIsArr = SK == kArr || SK == kArr8;
+
+// a + sign_extend(byte B of w), one VALU op
+template <int B>
+__device__ __forceinline__ int add_sbyte(int a, int w)
+{
+    int r;
+    if constexpr (B == 0) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(a), "v"(w));
+    else if constexpr (B == 1) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(a), "v"(w));
+    else if constexpr (B == 2) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(a), "v"(w));
+    else asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(a), "v"(w));
+    return r;
+}
+
+// Text-code dwords per body: one per step, or one per four steps (kArr8).
+template <int R, int SK>
+struct Codes {
+    static constexpr int NT = SK == kArr8 ? Cfg<R>::U / 4 : Cfg<R>::U;
+};
 
 // One unrolled body of U steps. Body kinds (KIND):
 //   kSteady  every lane is on a column >= 1. Lanes past column n compute garbage, which is harmless:
 //            it only ever flows to lanes that are past n as well, their direction planes are never
-//            read, their bottom-row values are never published and their local best-cell keys are
+//            read, their bottom-row values are never read and their local best-cell keys are
 //            filtered by column; only the global score and the local best-cell keys need the exact
 //            final state (kGeneric).
-//   kStart   the first bodies (s < 63): lane k is still left of column 1 while s < k. Forcing the
-//            substitution score of those virtual cells to 0 keeps their state at the boundary
-//            value 0 (F = max(0+0, 0, 0); H = max(0+0, -g, -g, 0)), so lane k enters column 1 with
-//            exactly the column-0 state: one compare + one select per cell instead of masking all
-//            of the state. (kArr strips need no kStart bodies: their padding scores are 0.)
-//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row).
+//   kStart   the first bodies (s < 63, kProf / kTable only): lane k is still left of column 1 while
+//            s < k. Forcing the substitution score of those virtual cells to 0 keeps their state at
+//            the boundary value (see the recurrences), so lane k enters column 1 with exactly the
+//            column-0 state. Text profiles need no kStart bodies: their padding scores are 0.
+//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row, and
+//            local strips' last bodies).
 enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
+// Recurrences (per lane-row; diag/up/left are the neighbours' values):
+//   global, shifted domain F = H + g(i+j): F = max(Fdiag + S + 2g, Fleft, Fup), boundaries 0;
+//     DIAG iff Fdiag + S + 2g > max(Fleft, Fup); plane 1 = raw "up > left".
+//   local, H with the gap folded into the score: X = max(Hdiag + S + g, max(Hleft, Hup)),
+//     H = max(X - g, 0) (one saturating subtraction: X >= 0); DIAG iff Hdiag + S + g > max(Hleft,
+//     Hup) (the reference's D > max(L, U) with every candidate shifted by +g); raw TOP iff Hup >
+//     Hleft; STOP iff H == 0 (alignSequenceCPU.cpp:175-190).
 // Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
 // wave_shr:1 whose `old` operand is this step's feed register Q (lane 0 keeps Q's lane 0 = the
 // strip above's bottom value for this column); Q is dead afterwards, so the DPP writes in place. The
@@ -242,21 +274,19 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // stays in its own register Fs[q] until the body ends, when lane 63 publishes all U of them.
 template <int R, bool LOCAL, int SK, int KIND>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
-                                         int kb, const int (&prof)[R], const int (&T)[Cfg<R>::U],
-                                         int (&F)[R], int (&G)[R], int (&best)[R], int &upPrev, int Q,
+                                         int kb, const int (&prof)[R], const int (&T)[Codes<R, SK>::NT],
+                                         int (&F)[R], int (&best)[R], int &upPrev, int Q,
                                          int (&Fs)[Cfg<R>::U], uint32_t (&acc)[3][Cfg<R>::NW])
 {
     constexpr int U = Cfg<R>::U;
     sfor<U>([&](auto Qc) {
         constexpr int q = decltype(Qc)::value;
         const int s = s0 + q;
-        const int t = T[q];
         const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
         int up = dpp_shr1(Q, F[R - 1]);
         Q = Qn;
         int diag = upPrev;
         upPrev = up;
-        int gu = up - g;  // local only
         constexpr bool RAMP = KIND == kGeneric;
         bool act = true;
         if constexpr (RAMP)
@@ -270,51 +300,39 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
         sfor<R>([&](auto Rc) {
             constexpr int rho = decltype(Rc)::value;
             constexpr int w = ((q * R + rho) / 32) % Cfg<R>::NW;
-            int sc;
-            if constexpr (SK == kArr) sc = t;
-            else if constexpr (SK == kProf) sc = __builtin_amdgcn_sbfe(prof[rho], t, 8);
-            else sc = ldsS[prof[rho] + t];
-            if constexpr (KIND == kStart) sc = real ? sc : 0;
+            int D;
+            if constexpr (SK == kArr8) D = add_sbyte<q & 3>(diag, T[q >> 2]);
+            else
+            {
+                int sc;
+                if constexpr (SK == kArr) sc = T[q];
+                else if constexpr (SK == kProf) sc = __builtin_amdgcn_sbfe(prof[rho], T[q], 8);
+                else sc = ldsS[prof[rho] + T[q]];
+                if constexpr (KIND == kStart) sc = real ? sc : 0;
+                D = diag + sc;
+            }
+            const int left = F[rho];
+            const int M = max(left, up);
+            acc[0][w] = push_sign(acc[0][w], M - D);      // DIAG
+            acc[1][w] = push_sign(acc[1][w], left - up);  // raw "up > left" (global) / raw TOP (local)
+            int Fn;
             if constexpr (!LOCAL)
             {
-                const int left = F[rho];
-                const int D = diag + sc;
-                const int M = max(left, up);
-                int Fn = max(D, M);
-                acc[0][w] = push_sign(acc[0][w], M - D);     // DIAG
-                acc[1][w] = push_sign(acc[1][w], left - up); // up > left
-                if constexpr (RAMP) Fn = act ? Fn : left;
-                diag = left;
-                up = Fn;
-                F[rho] = Fn;
+                Fn = max(D, M);
             }
             else
             {
-                const int Hl = F[rho], Gl = G[rho];
-                const int D = diag + sc;
-                const int M = max(Gl, gu);
-                int Hn = max(max(D, M), 0);
-                acc[0][w] = push_sign(acc[0][w], M - D);     // DIAG
-                acc[1][w] = push_sign(acc[1][w], Gl - gu);   // raw TOP
-                acc[2][w] = push_sign(acc[2][w], Hn - 1);    // STOP (H == 0)
-                int Gn = Hn - g;
-                const int key = (Hn << kb) + Ks;
-                if constexpr (RAMP)
-                {
-                    best[rho] = act ? max(best[rho], key) : best[rho];
-                    Hn = act ? Hn : Hl;
-                    Gn = act ? Gn : Gl;
-                }
-                else
-                {
-                    best[rho] = max(best[rho], key);
-                }
-                diag = Hl;
-                up = Hn;
-                gu = Gn;
-                F[rho] = Hn;
-                G[rho] = Gn;
+                const unsigned X = (unsigned)max(D, M);
+                Fn = (int)__builtin_elementwise_sub_sat(X, (unsigned)g);
+                acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
+                const int key = (Fn << kb) + Ks;
+                if constexpr (RAMP) best[rho] = act ? max(best[rho], key) : best[rho];
+                else best[rho] = max(best[rho], key);
             }
+            if constexpr (RAMP) Fn = act ? Fn : left;
+            diag = left;
+            up = Fn;
+            F[rho] = Fn;
         });
         Fs[q] = F[R - 1];
     });
@@ -353,10 +371,15 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
     }
 }
 
-template <int R, bool LOCAL, int SK>
+// One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
+// compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
+// codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
+// kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
+template <int R, bool LOCAL, int SK, bool HP, bool HN>
 __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
+    constexpr int NT = Codes<R, SK>::NT;
     const StripDesc sd = a.strips[idx];
     const PairDesc pd = a.pairs[sd.pair];
     const int n = (int)pd.text_len, m = (int)pd.pattern_len;
@@ -371,10 +394,19 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         c = min(max(c, 0), a.A - 1);
         prof[rho] = SK == kProf ? a.prof_tab[c] : SK == kTable ? c * a.A : c;
     });
-    // kArr: this lane's row letter selects its text profile (R = 1)
-    const int32_t *codes = a.codes + pd.code_off + (SK == kArr ? (uint64_t)prof[0] * pd.code_len : 0) + kPad;
-    const bool hasPrev = (sd.flags & kHasPrev) != 0;
-    const bool hasNext = (sd.flags & kHasNext) != 0;
+    // lane k at step s needs the score / code of column s-k+1: text index s - k
+    const int32_t *codes;
+    if constexpr (SK == kArr8)
+    {
+        // byte copy r = k % 4 of letter a: byte kPad + x holds S[a][t[x - r]]; read from x = s0 - (k & ~3)
+        const int8_t *b8 = reinterpret_cast<const int8_t *>(a.codes + pd.code_off) +
+                           ((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3);
+        codes = reinterpret_cast<const int32_t *>(b8);
+    }
+    else if constexpr (SK == kArr)
+        codes = a.codes + pd.code_off + (uint64_t)prof[0] * pd.code_len + kPad - lane;
+    else
+        codes = a.codes + pd.code_off + kPad - lane;
     lds_int *rin = (lds_int *)(rings + w * kRing);
     lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
     lds_int *progIn = (lds_int *)&H.prog[w];
@@ -397,23 +429,22 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     const bool needFinal = LOCAL || (m - sd.row0 >= 0 && m - sd.row0 < kWave * R);
 
     // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
-    int F[R], G[R], best[R];
+    int F[R], best[R];
     sfor<R>([&](auto Rc) {
         constexpr int rho = decltype(Rc)::value;
         F[rho] = 0;
-        G[rho] = -g;
         best[rho] = 0;
     });
     int upPrev = 0, Q = 0;
     int Fs[U];
-    // text codes, double-buffered across the two bodies of one loop trip (no register copies);
-    // lane k at step s needs the code of column s-k+1, i.e. codes[s - k]
-    int TA[U], TB[U];
-    auto load_codes = [&](int s0, int (&dst)[U]) __attribute__((always_inline)) {
+    // text codes, double-buffered across the two bodies of a pair (no register copies)
+    int TA[NT], TB[NT];
+    auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
-        sfor<U / 4>([&](auto Qc) {
+        const int32_t *src = SK == kArr8 ? codes + s0 / 4 : codes + s0;
+        sfor<NT / 4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value * 4;
-            const i32x4u v = *(const i32x4u *)(codes + s0 + q - lane);
+            const i32x4u v = *(const i32x4u *)(src + q);
             dst[q] = v.x;
             dst[q + 1] = v.y;
             dst[q + 2] = v.z;
@@ -425,89 +456,58 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     bool ok = true;
     int avail = 0;       // columns known to be in rin
     int consKnown = 0;   // columns the consumer of rout is known to have read
-    // lanes 0..U-1 take the bottom values of columns base+1 .. base+U of the strip above. The
-    // progress word and the values are read speculatively one body ahead (LDS is in order: values
-    // read after a progress word that covers them are valid), so a feed that is already there
-    // costs no LDS round trip at the body boundary.
+    // The progress word and the feed values for body k+2 are read speculatively at the end of body
+    // k and used at the end of body k+1 without an LDS round trip (LDS is in order per wave: values
+    // read after a progress word that covers them are valid). At a body boundary the order is feed
+    // check -> publish -> consumption word -> next prefetch, so the boundary's only LDS wait (the
+    // feed check) never waits for the boundary's own writes. Feeds and publications are not masked
+    // at the ends of the text: values of columns <= 0 or > n only ever reach cells outside [1, n].
     int pfProg = 0, pfVal = 0;
-    auto prefetch_feed = [&](int base) __attribute__((always_inline)) {
-        if (!hasPrev) return;
-        pfProg = lds_ld(progIn);
-        pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
-    };
-    auto feed = [&](int base) __attribute__((always_inline)) -> bool {  // (hasPrev only)
-        const int need = min(n, base + U);
-        if (uniform(pfProg) >= need)
+    auto prefetch = [&](int base) __attribute__((always_inline)) {
+        if constexpr (HP)
         {
-            avail = uniform(pfProg);
+            pfProg = lds_ld(progIn);
+            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
         }
-        else
+    };
+    // lanes 0..U-1 of Q take the bottom values of columns base+1 .. base+U of the strip above
+    auto feed = [&](int base) __attribute__((always_inline)) -> bool {
+        if constexpr (!HP)
+        {
+            // row 0 boundary. The zero is opaque on purpose: with a known-zero `old` the compiler
+            // folds the up-DPP into its consumers with bound_ctrl:1, and on gfx950 wave_shr with
+            // bound_ctrl does not hand lane 0 a zero (measured: wrong row 1 in strip 0)
+            asm volatile("v_mov_b32 %0, 0" : "=v"(Q));
+            return true;
+        }
+        const int need = min(n, base + U);
+        if (__builtin_expect(uniform(pfProg) < need, 0))
         {
             if (!wait_ring(a, progIn, need, avail, lane)) return false;
             pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
         }
-        Q = base + lane < n ? pfVal : 0;  // lanes >= U: don't care
-        if (lane == 0) lds_st(consIn, base + U);
+        Q = pfVal;  // lanes >= U: don't care
         return true;
     };
-    prefetch_feed(0);
-    if (hasPrev) ok = feed(0);
+    auto consumed = [&](int upto) __attribute__((always_inline)) {
+        if constexpr (HP)
+            if (lane == 0) lds_st(consIn, upto);
+    };
+    prefetch(0);
+    ok = feed(0);
+    consumed(U);
+    prefetch(U);
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
-    int published = 0;
     uint64_t lbest = 0;
-    auto body = [&](int s0, int (&T)[U], int (&Tn)[U]) __attribute__((always_inline)) -> bool {
+    auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) -> bool {
+        constexpr int KIND = decltype(kind)::value;
         const int s1 = s0 + U;
-        load_codes(s1, Tn);  // prefetch one body ahead
-        if (s1 < nSteps) prefetch_feed(s1);
-        if (needFinal && s1 > n)
-            run_body<R, LOCAL, SK, kGeneric>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
-        else if (SK != kArr && s0 < kWave - 1)
-            run_body<R, LOCAL, SK, kStart>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
-        else
-            run_body<R, LOCAL, SK, kSteady>(H.S, s0, lane, n, g, kb, prof, T, F, G, best, upPrev, Q, Fs, acc);
-        // a chunk is complete after BPC bodies: s1*R slots done, a multiple of CS
-        if (Cfg<R>::BPC == 1 || ((s1 * R) & (Cfg<R>::CS - 1)) == 0)
+        load_codes(s1, Tn);  // one body ahead
+        run_body<R, LOCAL, SK, KIND>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, Fs, acc);
+        if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
             store_chunk<R, LOCAL>(mk + (size_t)chunk * (kWave * Cfg<R>::LW), acc);
-        }
-        if (hasNext)
-        {
-            // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
-            // columns <= 0 are ramp garbage that lands in ring slots of columns far ahead (never
-            // yet published), columns > n are never read
-            const int c0 = s0 - (kWave - 2);
-            const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
-            if (c0 + U - 1 >= 1 && c0 <= n)
-            {
-                // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
-                if (c0 + U - 1 - kRing > consKnown)
-                {
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    for (uint32_t spin = 1;; ++spin)
-                    {
-                        consKnown = uniform(lds_ld(consOut));
-                        if (c0 + U - 1 - kRing <= consKnown) break;
-                        __builtin_amdgcn_s_sleep(1);
-                        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
-                    }
-                }
-                if (lane == kWave - 1)
-                {
-                    typedef int i32x4 __attribute__((ext_vector_type(4)));
-                    typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
-                    lds_i32x4 *dst = (lds_i32x4 *)(rout + ring_slot(c0));
-                    sfor<U / 4>([&](auto Xc) {
-                        constexpr int x = decltype(Xc)::value;
-                        dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
-                    });
-                }
-                // the values go before the progress word: a compiler-only fence (LDS executes one
-                // wave's operations in order)
-                asm volatile("" ::: "memory");
-            }
-            if (lane == kWave - 1 && top > published) lds_st(progOut, top);
-            published = top;
         }
         if constexpr (LOCAL)
         {
@@ -533,20 +533,69 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 });
             }
         }
-        if (s1 >= nSteps) return true;
-        if (!hasPrev)
+        // (after the last body this waits for the strip above's final progress word, n)
+        if (!feed(s1)) return false;
+        if constexpr (HN)
         {
-            Q = 0;  // row 0 boundary
-            return true;
+            // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
+            // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
+            const int c0 = s0 - (kWave - 2);
+            const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
+            if (__builtin_expect(c0 + U - 1 - kRing > consKnown, 0))
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    consKnown = uniform(lds_ld(consOut));
+                    if (c0 + U - 1 - kRing <= consKnown) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+                }
+            }
+            if (lane == kWave - 1)
+            {
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
+                lds_i32x4 *dst = (lds_i32x4 *)(rout + ring_slot(c0));
+                sfor<U / 4>([&](auto Xc) {
+                    constexpr int x = decltype(Xc)::value;
+                    dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
+                });
+                // the values go before the progress word: a compiler-only fence (LDS executes one
+                // wave's operations in order)
+                asm volatile("" ::: "memory");
+                lds_st(progOut, top);
+            }
         }
-        return feed(s1);
+        consumed(s1 + U);
+        prefetch(s1 + U);
+        return true;
     };
-    for (int s0 = 0; ok && s0 < nSteps; s0 += 2 * U)
+    using KSteady = std::integral_constant<int, kSteady>;
+    using KStart = std::integral_constant<int, kStart>;
+    using KGeneric = std::integral_constant<int, kGeneric>;
+    using First = std::false_type;
+    using Second = std::true_type;
+    // tail pairs: from the first pair holding a body with s1 > n (only where the final state is read)
+    const int sTail = needFinal ? max(0, (n - 2 * U + 1 + 2 * U - 1) / (2 * U) * (2 * U)) : nSteps;
+    int s0 = 0;
+    if constexpr (!kIsArr<SK>)
+        for (; ok && s0 < min(kWave, sTail); s0 += 2 * U)
+        {
+            ok = body(KStart{}, First{}, s0, TA, TB);
+            if (ok) ok = body(KStart{}, Second{}, s0 + U, TB, TA);
+        }
+    for (; ok && s0 < sTail; s0 += 2 * U)
     {
-        ok = body(s0, TA, TB);
-        if (ok) ok = body(s0 + U, TB, TA);
+        ok = body(KSteady{}, First{}, s0, TA, TB);
+        if (ok) ok = body(KSteady{}, Second{}, s0 + U, TB, TA);
     }
-    if (hasNext && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
+    for (; ok && s0 < nSteps; s0 += 2 * U)
+    {
+        ok = body(KGeneric{}, First{}, s0, TA, TB);
+        if (ok) ok = body(KGeneric{}, Second{}, s0 + U, TB, TA);
+    }
+    if (HN && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
     if (a.timeline && lane == 0)
     {
         uint64_t *tl = a.timeline + 4 * (size_t)idx;
@@ -659,7 +708,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK>
+template <int R, bool LOCAL, int SK, bool CHAIN>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -667,7 +716,9 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
     lds_int *rings = (lds_int *)(lds_dyn + sizeof(GroupHdr) / 4);
     const int lane = threadIdx.x & (kWave - 1);
     const int w = uniform((int)(threadIdx.x / kWave));
-    const int W = (int)(blockDim.x / kWave) - 1;  // compute waves; wave W is the I/O wave
+    // compute waves; with CHAIN wave W is the I/O wave (plans without strip chains have none, and no
+    // rings in LDS either: more workgroups fit a CU)
+    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0);
     if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
     while (true)
@@ -686,23 +737,92 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         __syncthreads();
         const int grp = uniform(H.group);
         if (grp >= a.num_groups) break;
-        if (w == W)
+        if (CHAIN && w == W)
         {
             io_wave(a, H, rings, grp, W, lane);
         }
         else
         {
             const int idx = grp * W + w;
-            if (idx < a.num_strips) process_strip<R, LOCAL, SK>(a, H, rings, idx, w, lane);
+            if (idx < a.num_strips)
+            {
+                // the strip kind is compile-time inside process_strip (branch-free body boundaries)
+                // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
+                // variant is instantiated, which keeps the register count of the batch kernel down)
+                const int f = uniform(a.strips[idx].flags) & (kHasPrev | kHasNext);
+                if constexpr (CHAIN)
+                {
+                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, H, rings, idx, w, lane);
+                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, H, rings, idx, w, lane);
+                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, H, rings, idx, w, lane);
+                    else process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                }
+                else
+                {
+                    (void)f;
+                    process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                }
+            }
         }
     }
 }
 
-// Text codes for the fill: one dword per letter, 8*c (packed profile bit offset) or c (LDS table
-// index). With text profiles (R = 1) the pair's block holds A arrays of code_len dwords instead,
-// array a = the scores S[a][t[x]] (+2g for global) of row letter a against every text letter.
-__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int scale,
-                                   const int32_t *table, int profiles)
+// Fill launches, one translation unit per strip height R (fill_r<R>.hip instantiates
+// launch_fill_r<R>; the main unit only declares them), so the 48 fill kernels compile in parallel.
+template <int R, bool LOCAL, int SK>
+void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t st)
+{
+    if (chain) hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
+    else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
+}
+
+// R = 1 uses text profiles (kArr8 when the scores fit int8, kArr otherwise); taller strips use the
+// packed profile when the scores fit (kProf) and the LDS table otherwise (kTable).
+template <int R>
+void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st)
+{
+    if constexpr (R == 1)
+    {
+        if (sk == kArr8)
+        {
+            if (local) launch_fill_t<1, true, kArr8>(a, grid, W, chain, st);
+            else launch_fill_t<1, false, kArr8>(a, grid, W, chain, st);
+        }
+        else
+        {
+            if (local) launch_fill_t<1, true, kArr>(a, grid, W, chain, st);
+            else launch_fill_t<1, false, kArr>(a, grid, W, chain, st);
+        }
+    }
+    else if (local)
+    {
+        if (sk == kProf) launch_fill_t<R, true, kProf>(a, grid, W, chain, st);
+        else launch_fill_t<R, true, kTable>(a, grid, W, chain, st);
+    }
+    else
+    {
+        if (sk == kProf) launch_fill_t<R, false, kProf>(a, grid, W, chain, st);
+        else launch_fill_t<R, false, kTable>(a, grid, W, chain, st);
+    }
+}
+
+#ifdef SA_FILL_R
+template void launch_fill_r<SA_FILL_R>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+}  // namespace sa
+#else
+extern template void launch_fill_r<1>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+extern template void launch_fill_r<2>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+extern template void launch_fill_r<4>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+extern template void launch_fill_r<8>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+extern template void launch_fill_r<16>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+extern template void launch_fill_r<32>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+
+// Text codes for the fill (layout per score kind, see ScoreKind):
+//   kProf / kTable  one dword per letter, 8*c (packed-profile bit offset) or c (LDS table index);
+//   kArr            A dword arrays of code_len: array a holds table[a][t[x]] at kPad + x;
+//   kArr8           4A byte arrays of code_len bytes: copy (a, r) holds table[a][t[x]] at kPad + x + r.
+__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int SK,
+                                   const int32_t *table)
 {
     const PairDesc pd = pairs[blockIdx.y];
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
@@ -710,10 +830,16 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
     {
         int c = text[pd.text_off + x];
         c = min(max(c, 0), A - 1);
-        if (profiles)
+        if (SK == kArr8)
+        {
+            int8_t *b8 = reinterpret_cast<int8_t *>(codes + pd.code_off);
+            for (int r = 0; r < A; ++r)
+                for (int sh = 0; sh < 4; ++sh) b8[((uint64_t)r * 4 + sh) * pd.code_len + kPad + x + sh] = (int8_t)table[r * A + c];
+        }
+        else if (SK == kArr)
             for (int r = 0; r < A; ++r) codes[pd.code_off + (uint64_t)r * pd.code_len + kPad + x] = table[r * A + c];
         else
-            codes[pd.code_off + kPad + x] = c * scale;
+            codes[pd.code_off + kPad + x] = SK == kProf ? 8 * c : c;
     }
 }
 
@@ -1066,7 +1192,8 @@ int dmalloc(T **p, size_t bytes)
 struct sa_plan {
     int device = 0;
     int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12;
-    bool packed = false;
+    int sk = 0;          // ScoreKind of the fill
+    bool chain = false;  // some pair has more than one strip
     int num_cu = 0;
     std::vector<PairDesc> pairs;
     std::vector<StripDesc> strips;
@@ -1122,50 +1249,20 @@ int choose_W(const std::vector<PairDesc> &pairs)
         const int w = std::atoi(e);
         if (w >= 1 && w <= kMaxWaves) return w;
     }
-    for (const PairDesc &d : pairs)
-        if (d.num_strips > 1) return 4;
-    return 1;
+    (void)pairs;
+    return 4;
 }
 
-template <int R, bool LOCAL, int SK>
-void launch_fill_t(const FillArgs &a, int grid, int W, hipStream_t st)
-{
-    hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
-}
-
-// R = 1 always uses text profiles (kArr); taller strips use the packed profile when the scores fit
-// (kProf) and the LDS table otherwise (kTable).
-template <int R>
-void launch_fill_r(const FillArgs &a, bool local, bool packed, int grid, int W, hipStream_t st)
-{
-    if constexpr (R == 1)
-    {
-        (void)packed;
-        if (local) launch_fill_t<1, true, kArr>(a, grid, W, st);
-        else launch_fill_t<1, false, kArr>(a, grid, W, st);
-    }
-    else if (local)
-    {
-        if (packed) launch_fill_t<R, true, kProf>(a, grid, W, st);
-        else launch_fill_t<R, true, kTable>(a, grid, W, st);
-    }
-    else
-    {
-        if (packed) launch_fill_t<R, false, kProf>(a, grid, W, st);
-        else launch_fill_t<R, false, kTable>(a, grid, W, st);
-    }
-}
-
-void launch_fill(int R, const FillArgs &a, bool local, bool packed, int grid, int W, hipStream_t st)
+void launch_fill(int R, const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st)
 {
     switch (R)
     {
-    case 1: launch_fill_r<1>(a, local, packed, grid, W, st); break;
-    case 2: launch_fill_r<2>(a, local, packed, grid, W, st); break;
-    case 4: launch_fill_r<4>(a, local, packed, grid, W, st); break;
-    case 8: launch_fill_r<8>(a, local, packed, grid, W, st); break;
-    case 16: launch_fill_r<16>(a, local, packed, grid, W, st); break;
-    default: launch_fill_r<32>(a, local, packed, grid, W, st); break;
+    case 1: launch_fill_r<1>(a, local, sk, grid, W, chain, st); break;
+    case 2: launch_fill_r<2>(a, local, sk, grid, W, chain, st); break;
+    case 4: launch_fill_r<4>(a, local, sk, grid, W, chain, st); break;
+    case 8: launch_fill_r<8>(a, local, sk, grid, W, chain, st); break;
+    case 16: launch_fill_r<16>(a, local, sk, grid, W, chain, st); break;
+    default: launch_fill_r<32>(a, local, sk, grid, W, chain, st); break;
     }
 }
 
@@ -1225,6 +1322,9 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     const int A = P->alphabet_size;
     if (A < 1 || A > 32) return fail(SA_ERR_INVALID, "alphabet_size must be 1..32");
     if (P->mode != SA_GLOBAL && P->mode != SA_LOCAL) return fail(SA_ERR_INVALID, "mode must be SA_GLOBAL or SA_LOCAL");
+    // the reference takes a positive gap penalty (utilities.cpp parseArguments); the local
+    // recurrence's saturating subtraction relies on g >= 0
+    if (P->gap_penalty < 0) return fail(SA_ERR_UNSUPPORTED, "gap_penalty must be >= 0");
     const int64_t g = P->gap_penalty;
     int64_t smax = INT32_MIN, smin = INT32_MAX, sabs = 0;
     for (int e = 0; e < A * A; ++e)
@@ -1258,13 +1358,16 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     pl->R = choose_R(P, pairs, np);
     pl->U = (16 / pl->R) > 4 ? 16 / pl->R : 4;
     pl->key_bits = std::min(12, std::max(4, 30 - bitlen(hmax_local)));
-    const int64_t off2 = P->mode == SA_GLOBAL ? 2 * g : 0;
-    pl->packed = A <= 4;
-    for (int e = 0; e < A * A && pl->packed; ++e)
+    // the tables hold S + 2g (global, shifted domain) or S + g (local), see run_body
+    const int64_t off2 = P->mode == SA_GLOBAL ? 2 * g : g;
+    bool fits8 = true;
+    for (int e = 0; e < A * A; ++e)
     {
         const int64_t v = P->score_matrix[e] + off2;
-        if (v < -128 || v > 127) pl->packed = false;
+        if (v < -128 || v > 127) fits8 = false;
     }
+    if (pl->R == 1) pl->sk = fits8 ? kArr8 : kArr;
+    else pl->sk = (A <= 4 && fits8) ? kProf : kTable;
     if (P->alphabet) std::memcpy(pl->alphabet, P->alphabet, std::min<size_t>(A + 1, 33));
     else for (int c = 0; c <= A; ++c) pl->alphabet[c] = c == A ? '-' : (char)('A' + c);
 
@@ -1288,8 +1391,9 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         d.pattern_off = pairs[p].pattern_offset;
         d.pattern_len = pairs[p].pattern_len;
         d.code_off = code_bytes;
-        d.code_len = kPad + d.text_len + 4 * kPad;
-        code_bytes += (R == 1 ? (uint64_t)A : 1) * d.code_len;  // R = 1: A text profiles
+        // kArr8: code_len bytes per copy (4A copies); kArr: A arrays of code_len dwords; else one
+        d.code_len = (kPad + d.text_len + 4 * kPad + 3) / 4 * 4;
+        code_bytes += pl->sk == kArr8 ? (uint64_t)A * d.code_len : pl->sk == kArr ? (uint64_t)A * d.code_len : d.code_len;
         d.out_off = outb;
         outb += d.text_len + d.pattern_len + 16;
         d.first_strip = (int32_t)pl->strips.size();
@@ -1316,11 +1420,12 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     pl->out_bytes = outb;
     pl->bytes_masks = mask_entries * 16;
     pl->W = choose_W(pl->pairs);
+    for (const PairDesc &d : pl->pairs) pl->chain = pl->chain || d.num_strips > 1;
 
     // ---- tables ----
     std::vector<int32_t> prof(4, 0), table(A * A);
     for (int e = 0; e < A * A; ++e) table[e] = (int32_t)(P->score_matrix[e] + off2);
-    if (pl->packed)
+    if (pl->sk == kProf)
         for (int cp = 0; cp < A; ++cp)
         {
             uint32_t w = 0;
@@ -1391,7 +1496,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             // pairs beyond 65535 are handled by re-basing the pair pointer
             const int cnt = std::min(65535, np - y0);
             hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
-                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->packed ? 8 : 1, pl->d_table, pl->R == 1 ? 1 : 0);
+                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->sk, pl->d_table);
         }
         HIP_TRY(hipGetLastError());
         if (int rc = debug_sync(st, "encode_text_kernel")) return rc;
@@ -1431,8 +1536,11 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         if (tlPath) HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * 4 * ns));
         const int W = pl->W;
         a.num_groups = (ns + W - 1) / W;
-        const int grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
-        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->packed, grid, W, st);
+        // chains: two workgroups of W compute waves + an I/O wave per CU; lone strips: W compute
+        // waves per workgroup and up to 16 waves per CU (the batch kernel stays under 128 VGPRs)
+        const int perCU = pl->chain ? std::max(1, 8 / W) : std::max(1, 16 / W);
+        const int grid = std::min(a.num_groups, std::max(1, pl->num_cu) * perCU);
+        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
         HIP_TRY(hipGetLastError());
         if (tlPath)
         {
@@ -1659,3 +1767,5 @@ int sa_selftest(int device)
 }
 
 }  // extern "C"
+
+#endif  // SA_FILL_R

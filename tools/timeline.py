@@ -70,6 +70,7 @@ def main():
         "lag_ns_by_strip": [round(float(x), 1) for x in lag[:: max(1, len(lag) // 16)]],
         "xcc_of_first_16": xcc[:16].tolist(),
         "cu_se_of_first_8": [(int(c), int(s)) for c, s in zip(cu[:8], se[:8])],
+        "simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in hw[:8]],
     }
     print(json.dumps(rec))
     b.close()
