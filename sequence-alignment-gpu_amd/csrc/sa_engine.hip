@@ -848,7 +848,10 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
 // ------------------------------------------------------------------------------------------------
 constexpr int kWinEntries = 512;   // entries (16 bytes each) per LDS window buffer: 2 x 8 KiB
 constexpr int kWinPerLane = kWinEntries / 64;
-constexpr int kNearTop = 8;        // rows below a strip's top at which the next strip is prefetched
+#ifndef SA_TB_NEARTOP
+#define SA_TB_NEARTOP 8
+#endif
+constexpr int kNearTop = SA_TB_NEARTOP;  // rows below a strip's top at which the next strip is prefetched
 
 struct TbArgs {
     const int8_t *text, *pattern;
@@ -860,27 +863,28 @@ struct TbArgs {
     uint8_t *ops;
     char *out_text, *out_pattern;
     sa_result *results;
+    uint64_t *timing;           // debug (SA_TB_TIMING): per pair {start, walk done, pass 1, pass 2}
     int32_t mode, gap, A;
     char alphabet[33];
 };
 
 enum { kLeft = 0, kDiag = 1, kTop = 2, kStop = 3 };  // SequenceAlignment.hpp:122
 
-template <int R>
+template <int R, int MODE>
 __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
 {
     __shared__ uint4 win[2][kWinEntries];
     __shared__ char alpha[40];
-    __shared__ int scan[2][kWave];
     constexpr int RB = kWave * R;
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     const PairDesc pd = a.pairs[p];
     const int n = (int)pd.text_len, m = (int)pd.pattern_len;
     if (lane < 33) alpha[lane] = a.alphabet[lane];
+    const uint64_t tT0 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
 
     int score, i, j;
-    if (a.mode == SA_GLOBAL)
+    if constexpr (MODE == SA_GLOBAL)
     {
         score = pd.num_strips > 0 ? a.pair_score[p] : -a.gap * (n + m);
         i = m;
@@ -967,7 +971,9 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         {
             if (!(b == pfStrip && e >= pfLo && e < pfLo + kWinEntries)) stage_load(b, e & ~(kWinEntries - 1));
             stage_commit();
+#ifndef SA_TB_NO_BELOW
             if (curLo > 0) stage_load(b, curLo - kWinEntries);
+#endif
         }
         if (il < kNearTop && b > 0 && pfStrip != b - 1)
             stage_load(b - 1, ((jj - 1 + kWave - 1) * R + R - 1) & ~(kWinEntries - 1));
@@ -984,7 +990,7 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         const int sh = 31 - (rel & 31);
         const int b0 = (int)((w0 >> sh) & 1u), b1 = (int)((w1 >> sh) & 1u);
         // global: plane1 is the raw "up > left" bit, DIAG wins; local: {DIAG|STOP, TOP&~DIAG|STOP}
-        return a.mode == SA_GLOBAL ? (b0 ? kDiag : (b1 ? kTop : kLeft)) : (b0 | (b1 << 1));
+        return MODE == SA_GLOBAL ? (b0 ? kDiag : (b1 ? kTop : kLeft)) : (b0 | (b1 << 1));
     };
     auto move = [&](int tt, int tp, int ni, int nj) __attribute__((always_inline)) {  // after i -= tp, j -= tt
         e -= (tt << LOG2R) + tp;
@@ -1003,11 +1009,11 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         if ((len & (kWave - 1)) == 0) ops[len - kWave + lane] = (uint8_t)opsAcc;
     };
     // text / pattern index of the first letter the walk emits (the start cell's)
-    const int ti0 = a.mode == SA_GLOBAL ? n - 1 : j - 1;
-    const int pi0 = a.mode == SA_GLOBAL ? m - 1 : i - 1;
+    const int ti0 = MODE == SA_GLOBAL ? n - 1 : j - 1;
+    const int pi0 = MODE == SA_GLOBAL ? m - 1 : i - 1;
     int ti, pi;
     if (i > 0 && j > 0) enter(i, j);
-    if (a.mode == SA_GLOBAL)
+    if constexpr (MODE == SA_GLOBAL)
     {
         // traceBackNW (alignSequenceCPU.cpp:64-114): row 0 forces LEFT, column 0 forces TOP
         ti = n - 1;
@@ -1070,48 +1076,66 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         r.start_pattern = (uint64_t)(int64_t)pi;
         a.results[p] = r;
     }
-    __syncthreads();
+    const uint64_t tT1 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
+    __syncthreads();  // the op bytes are visible to every lane (one wave: LDS / global order)
 
-    // ops (walk order, i.e. reversed) -> letters (forward order). Letters only depend on how many
-    // text / pattern letters the later part of the path consumed, so each lane converts one chunk.
-    const int chunk = (len + kWave - 1) / kWave;
-    const int c0 = min(len, lane * chunk), c1 = min(len, c0 + chunk);
-    int nt = 0, np = 0;
-    for (int t = c0; t < c1; ++t)
+    // ops (walk order, i.e. reversed) -> letters (forward order), 64 ops per block with one op per
+    // lane: the text / pattern index of op t is the start index minus the number of text / pattern
+    // letters the ops before it consumed, i.e. a running base minus an in-block exclusive count
+    // (ballot + mbcnt). kUnroll blocks per trip keep their loads in flight together.
+    const uint64_t tT2 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
     {
-        const int d = ops[t];
-        nt += (d == kDiag || d == kLeft);
-        np += (d == kDiag || d == kTop);
-    }
-    scan[0][lane] = nt;
-    scan[1][lane] = np;
-    __syncthreads();
-    int bt = 0, bp = 0;
-    for (int l = 0; l < lane; ++l) { bt += scan[0][l]; bp += scan[1][l]; }
-    const char GAPC = alpha[a.A];
-    char *ot = a.out_text + pd.out_off;
-    char *op = a.out_pattern + pd.out_off;
-    int xt = ti0 - bt, xp = pi0 - bp;
-#ifdef SA_TB_DEBUG
-    if (c0 < c1) printf("letters lane=%d c0=%d c1=%d len=%d xt=%d xp=%d ti0=%d pi0=%d\n", lane, c0, c1, len, xt, xp, ti0, pi0);
-#endif
-    for (int t = c0; t < c1; ++t)
-    {
-        const int d = ops[t];
-        const int tt = d == kDiag || d == kLeft;
-        const int tp = d == kDiag || d == kTop;
-#ifdef SA_TB_DEBUG
-        if ((tt && (xt < 0 || xt >= n)) || (tp && (xp < 0 || xp >= m)) || d > 3)
+        constexpr int kUnroll = 8;
+        const char GAPC = alpha[a.A];
+        char *ot = a.out_text + pd.out_off;
+        char *op = a.out_pattern + pd.out_off;
+        const int8_t *tx = a.text + pd.text_off;
+        const int8_t *px = a.pattern + pd.pattern_off;
+        int bt = ti0, bp = pi0;  // text / pattern index consumed by the next op
+        for (int t0 = 0; t0 < len; t0 += kWave * kUnroll)
         {
-            printf("BAD letter lane=%d t=%d d=%d xt=%d xp=%d n=%d m=%d len=%d\n", lane, t, d, xt, xp, n, m, len);
-            xt -= tt; xp -= tp;
-            continue;
+            int d[kUnroll];
+            sfor<kUnroll>([&](auto Uc) {
+                constexpr int u = decltype(Uc)::value;
+                const int t = t0 + u * kWave + lane;
+                d[u] = t < len ? ops[t] : kStop;
+            });
+            int xt[kUnroll], xp[kUnroll], ct[kUnroll], cp[kUnroll];
+            sfor<kUnroll>([&](auto Uc) {
+                constexpr int u = decltype(Uc)::value;
+                const bool tt = d[u] == kDiag || d[u] == kLeft;
+                const bool tp = d[u] == kDiag || d[u] == kTop;
+                const uint64_t mt = ballot(tt), mp = ballot(tp);
+                xt[u] = bt - (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mt, 0));
+                xp[u] = bp - (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mp >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mp, 0));
+                ct[u] = tt ? (int)tx[max(xt[u], 0)] : -1;
+                cp[u] = tp ? (int)px[max(xp[u], 0)] : -1;
+                bt -= __builtin_popcountll(mt);
+                bp -= __builtin_popcountll(mp);
+            });
+            sfor<kUnroll>([&](auto Uc) {
+                constexpr int u = decltype(Uc)::value;
+                const int t = t0 + u * kWave + lane;
+                if (t < len)
+                {
+                    ot[len - 1 - t] = ct[u] >= 0 ? alpha[ct[u]] : GAPC;
+                    op[len - 1 - t] = cp[u] >= 0 ? alpha[cp[u]] : GAPC;
+                }
+            });
         }
-#endif
-        ot[len - 1 - t] = tt ? alpha[(int)a.text[pd.text_off + xt]] : GAPC;
-        op[len - 1 - t] = tp ? alpha[(int)a.pattern[pd.pattern_off + xp]] : GAPC;
-        xt -= tt;
-        xp -= tp;
+    }
+    if (a.timing)
+    {
+        __syncthreads();
+        if (lane == 0)
+        {
+            uint64_t *tm = a.timing + 4 * (size_t)p;
+            tm[0] = tT0;
+            tm[1] = tT1;
+            tm[2] = tT2;
+            tm[3] = __builtin_amdgcn_s_memrealtime();
+
+        }
     }
 }
 
@@ -1266,17 +1290,24 @@ void launch_fill(int R, const FillArgs &a, bool local, int sk, int grid, int W, 
     }
 }
 
-void launch_tb(int R, const TbArgs &a, int np, hipStream_t st)
+template <int MODE>
+void launch_tb_m(int R, const TbArgs &a, int np, hipStream_t st)
 {
     switch (R)
     {
-    case 1: hipLaunchKernelGGL(traceback_kernel<1>, dim3(np), dim3(kWave), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(traceback_kernel<2>, dim3(np), dim3(kWave), 0, st, a); break;
-    case 4: hipLaunchKernelGGL(traceback_kernel<4>, dim3(np), dim3(kWave), 0, st, a); break;
-    case 8: hipLaunchKernelGGL(traceback_kernel<8>, dim3(np), dim3(kWave), 0, st, a); break;
-    case 16: hipLaunchKernelGGL(traceback_kernel<16>, dim3(np), dim3(kWave), 0, st, a); break;
-    default: hipLaunchKernelGGL(traceback_kernel<32>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((traceback_kernel<1, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((traceback_kernel<2, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((traceback_kernel<4, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((traceback_kernel<8, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((traceback_kernel<16, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
+    default: hipLaunchKernelGGL((traceback_kernel<32, MODE>), dim3(np), dim3(kWave), 0, st, a); break;
     }
+}
+
+void launch_tb(int R, const TbArgs &a, int np, hipStream_t st)
+{
+    if (a.mode == SA_GLOBAL) launch_tb_m<SA_GLOBAL>(R, a, np, st);
+    else launch_tb_m<SA_LOCAL>(R, a, np, st);
 }
 
 void free_plan(sa_plan *p)
@@ -1586,8 +1617,24 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     a.gap = pl->gap;
     a.A = pl->A;
     std::memcpy(a.alphabet, pl->alphabet, 33);
+    // SA_TB_TIMING=<file>: debug dump of per-pair phase timestamps (s_memrealtime, 100 MHz)
+    const char *tmPath = std::getenv("SA_TB_TIMING");
+    a.timing = nullptr;
+    if (tmPath) HIP_TRY(hipMalloc((void **)&a.timing, sizeof(uint64_t) * 4 * np));
     launch_tb(pl->R, a, np, st);
     HIP_TRY(hipGetLastError());
+    if (tmPath)
+    {
+        std::vector<uint64_t> tm(4 * (size_t)np);
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(tm.data(), a.timing, tm.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(a.timing));
+        if (FILE *f = std::fopen(tmPath, "wb"))
+        {
+            std::fwrite(tm.data(), 8, tm.size(), f);
+            std::fclose(f);
+        }
+    }
     if (int rc = debug_sync(st, "traceback_kernel")) return rc;
     HIP_TRY(hipSetDevice(cur));
     return SA_OK;
