@@ -223,8 +223,9 @@ static_assert(kRing % 16 == 0, "ring must hold whole bodies");
 //           per letter so that every lane's 16-byte load is dword aligned (lane k reads copy k%4);
 //           one global_load_dwordx4 serves a whole 16-step body and the byte is picked by the
 //           add itself (SDWA src1_sel:BYTE_q, sign-extended).
+//   kPair   pair-packed lone strips (fill_pair_kernel): per column the two pairs' column profiles.
 // The zero padding of the profiles keeps the ramp cells left of column 1 at the boundary value.
-enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3 };
+enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3, kPair = 4 };
 template <int SK>
 constexpr bool kIsArr = SK == kArr || SK == kArr8;
 
@@ -626,6 +627,196 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// pair-packed fill (global mode, lone strips, DNA-sized alphabets): two independent pairs of the same
+// shape in the two 16-bit halves of every register
+// ------------------------------------------------------------------------------------------------
+// The shifted-domain global recurrence only needs unsigned add / max and sign bits of differences,
+// so when every value fits u16 (0 <= S + 2g <= 255, (max S + 2g) * min(m, n) <= 65535: F is
+// non-negative and bounded by that) and every difference compared fits i16 (|M - D|, |left - up| <=
+// 2 (max S + 2g)), one v_pk_* instruction advances both pairs.
+//   * Scores: per text column the code block holds two "column profiles" {colA, colB}, byte r of
+//     colA = S[r][tA] + 2g (zero in the padding); each row keeps one fixed selector
+//     rA | 0x0c00 | (4 + rB) << 16 | 0x0c000000, and one v_perm_b32(colB, colA, sel) gives the row's
+//     two scores as u16 halves.
+//   * Direction bits: slot σ of a 16-slot group sits at bit 15 - σ of each half. Slots s and s+8
+//     (s < 8) are rows ρ and ρ+8 of the same step (R >= 16); one v_perm_b32 gathers the four sign
+//     bits (both pairs, both slots) onto byte MSBs (bits 15, 7, 31, 23), one shift by s moves them to
+//     15-s, 7-s, 31-s, 23-s, and one v_and_or_b32 inserts them: 3 VALU per 4 bits.
+//   * At the body's end v_perm_b32 splits the packed words back into each pair's ordinary 32-slot
+//     words, so the stored planes, the traceback and the decoders are exactly those of the unpacked
+//     kernel.
+// About 4.5 VALU per cell instead of 8.2.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as16(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <int R>
+__device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane)
+{
+    constexpr int U = Cfg<R>::U;
+    constexpr int SB = Cfg<R>::SB;      // slots per body (per pair)
+    constexpr int NP = SB / 16;         // packed words per plane per body
+    constexpr int NW = Cfg<R>::NW, LW = Cfg<R>::LW;
+    static_assert(R >= 16 && Cfg<R>::BPC == 1 && SB % 32 == 0, "pair kernel: R >= 16, a body is one chunk");
+    const StripDesc dA = a.strips[sA], dB = a.strips[sA + 1];
+    const PairDesc pA = a.pairs[dA.pair], pB = a.pairs[dB.pair];
+    const int n = (int)pA.text_len, m = (int)pA.pattern_len;
+    const int g = a.gap;
+    const int rowTop = 1 + lane * R;
+    uint32_t rsel[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        const int i = rowTop + rho;
+        const int cA = i <= m ? min(max((int)a.pattern[pA.pattern_off + i - 1], 0), a.A - 1) : 0;
+        const int cB = i <= m ? min(max((int)a.pattern[pB.pattern_off + i - 1], 0), a.A - 1) : 0;
+        rsel[rho] = (uint32_t)cA | 0x0c00u | ((uint32_t)(4 + cB) << 16) | 0x0c000000u;
+    });
+    // column profiles {colA, colB} per column, in pair A's code block (2 dwords per column)
+    const int32_t *codes = a.codes + pA.code_off + 2 * (kPad - lane);
+    uint32_t *mkA = a.masks + dA.mask_off * 4 + lane * LW;
+    uint32_t *mkB = a.masks + dB.mask_off * 4 + lane * LW;
+    const int nSteps = dA.nsteps;
+    uint32_t F[R];
+    sfor<R>([&](auto Rc) { F[decltype(Rc)::value] = 0; });
+    uint32_t upPrev = 0;
+    int Q;
+    int TA[2 * U], TB[2 * U];
+    auto load_codes = [&](int s0, int (&dst)[2 * U]) __attribute__((always_inline)) {
+        typedef int i32x4u __attribute__((ext_vector_type(4), aligned(8)));
+        sfor<U / 2>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value * 4;
+            const i32x4u v = *(const i32x4u *)(codes + 2 * s0 + q);
+            dst[q] = v.x;
+            dst[q + 1] = v.y;
+            dst[q + 2] = v.z;
+            dst[q + 3] = v.w;
+        });
+    };
+    load_codes(0, TA);
+    auto body = [&](auto kind, int s0, int (&T)[2 * U], int (&Tn)[2 * U]) __attribute__((always_inline)) {
+        constexpr bool RAMP = decltype(kind)::value;  // tail: lanes outside [1, n] keep their state
+        const int s1 = s0 + U;
+        load_codes(s1, Tn);
+        uint32_t acc[2][NP];
+        asm volatile("v_mov_b32 %0, 0" : "=v"(Q));  // row 0 boundary (opaque zero: see feed())
+        sfor<U>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
+            uint32_t up = (uint32_t)dpp_shr1(Q, (int)F[R - 1]);
+            Q = Qn;
+            uint32_t diag = upPrev;
+            upPrev = up;
+            bool act = true;
+            if constexpr (RAMP)
+            {
+                const int c = s0 + q - lane;
+                act = (c >= 0) && (c < n);
+            }
+            const uint32_t colA = (uint32_t)T[2 * q], colB = (uint32_t)T[2 * q + 1];
+            uint32_t x0[R], x1[R];
+            sfor<R>([&](auto Rc) {
+                constexpr int rho = decltype(Rc)::value;
+                const uint32_t sc = __builtin_amdgcn_perm(colB, colA, rsel[rho]);
+                const u16x2 D = as16(diag) + as16(sc);
+                const uint32_t left = F[rho];
+                const u16x2 M = __builtin_elementwise_max(as16(left), as16(up));
+                uint32_t Fn = as32(__builtin_elementwise_max(D, M));
+                x0[rho] = as32(M - D);                     // DIAG iff sign
+                x1[rho] = as32(as16(left) - as16(up));     // up > left iff sign
+                if constexpr (RAMP) Fn = act ? Fn : left;
+                diag = left;
+                up = Fn;
+                F[rho] = Fn;
+                // rows rho-8 and rho of a 16-row group are slots s and s+8 of packed word w: insert
+                // as soon as both exist (keeps at most 8 rows of differences live)
+                if constexpr (rho % 16 >= 8)
+                {
+                    constexpr int sl = rho % 16 - 8;
+                    constexpr int w = (q * R + rho) / 16;
+                    constexpr uint32_t mask = (0x80808080u >> sl);
+                    const uint32_t y0 = __builtin_amdgcn_perm(x0[rho - 8], x0[rho], 0x07030501u) >> sl;
+                    const uint32_t y1 = __builtin_amdgcn_perm(x1[rho - 8], x1[rho], 0x07030501u) >> sl;
+                    if constexpr (sl == 0)
+                    {
+                        acc[0][w] = y0 & mask;
+                        acc[1][w] = y1 & mask;
+                    }
+                    else
+                    {
+                        acc[0][w] |= y0 & mask;
+                        acc[1][w] |= y1 & mask;
+                    }
+                }
+            });
+        });
+        // split the packed words into each pair's 32-slot words: {plane 0 words, plane 1 words}
+        const int chunk = (s1 * R) / Cfg<R>::CS - 1;
+        uint32_t vA[LW], vB[LW];
+        sfor<NW>([&](auto Wc) {
+            constexpr int w = decltype(Wc)::value;
+            sfor<2>([&](auto Pc) {
+                constexpr int p = decltype(Pc)::value;
+                vA[p * NW + w] = __builtin_amdgcn_perm(acc[p][2 * w], acc[p][2 * w + 1], 0x05040100u);
+                vB[p * NW + w] = __builtin_amdgcn_perm(acc[p][2 * w], acc[p][2 * w + 1], 0x07060302u);
+            });
+        });
+        uint32_t *dA_ = mkA + (size_t)chunk * (kWave * LW);
+        uint32_t *dB_ = mkB + (size_t)chunk * (kWave * LW);
+        sfor<LW / 4>([&](auto Xc) {
+            constexpr int x = decltype(Xc)::value;
+            *reinterpret_cast<u32x4 *>(dA_ + 4 * x) = u32x4{vA[4 * x], vA[4 * x + 1], vA[4 * x + 2], vA[4 * x + 3]};
+            *reinterpret_cast<u32x4 *>(dB_ + 4 * x) = u32x4{vB[4 * x], vB[4 * x + 1], vB[4 * x + 2], vB[4 * x + 3]};
+        });
+    };
+    // tail pairs of bodies from the first pair holding a body with s1 > n (the global score row is
+    // in every lone strip)
+    const int sTail = max(0, n / (2 * U) * (2 * U));
+    int s0 = 0;
+    for (; s0 < sTail; s0 += 2 * U)
+    {
+        body(std::false_type{}, s0, TA, TB);
+        body(std::false_type{}, s0 + U, TB, TA);
+    }
+    for (; s0 < nSteps; s0 += 2 * U)
+    {
+        body(std::true_type{}, s0, TA, TB);
+        body(std::true_type{}, s0 + U, TB, TA);
+    }
+    const int rm = m - 1;  // strip-relative row of the last DP row
+    if (lane == rm / R)
+    {
+        uint32_t v = F[0];
+        sfor<R>([&](auto Rc) {
+            constexpr int rho = decltype(Rc)::value;
+            if (rho == rm % R) v = F[rho];
+        });
+        a.pair_score[dA.pair] = (int)(v & 0xffffu) - g * (m + n);
+        a.pair_score[dB.pair] = (int)(v >> 16) - g * (m + n);
+    }
+}
+
+// One wave per two strips (pairs sA, sA+1); 4 waves per workgroup; dynamic queue over strip pairs.
+template <int R>
+__global__ __launch_bounds__(kWave * kMaxWaves, 2) void fill_pair_kernel(FillArgs a)
+{
+    __shared__ int unit;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = uniform((int)(threadIdx.x / kWave));
+    const int W = (int)(blockDim.x / kWave);
+    const int units = a.num_strips / 2;
+    while (true)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) unit = (int)atomicAdd(&a.ctrl->queue_head, 1u);
+        __syncthreads();
+        const int grp = uniform(unit);
+        if (grp * W >= units) break;
+        const int u = grp * W + w;
+        if (u < units) process_pair<R>(a, 2 * u, lane);
+    }
+}
+
 // The I/O wave of a group: global granules of the previous group's last strip -> ring[0], and
 // ring[W'] (W' = compute waves with a strip) -> granules for the next group. Only lane 0 polls the
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
@@ -794,6 +985,11 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
             else launch_fill_t<1, false, kArr>(a, grid, W, chain, st);
         }
     }
+    else if (sk == kPair)
+    {
+        if constexpr (R >= 16)
+            hipLaunchKernelGGL(fill_pair_kernel<R>, dim3(grid), dim3(kWave * W), 0, st, a);
+    }
     else if (local)
     {
         if (sk == kProf) launch_fill_t<R, true, kProf>(a, grid, W, chain, st);
@@ -825,6 +1021,31 @@ __global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, in
                                    const int32_t *table)
 {
     const PairDesc pd = pairs[blockIdx.y];
+    if (SK == kPair)
+    {
+        // selectors of pairs (2q, 2q+1) in pair 2q's block, padding included (0x0c0c0c0c = zeros)
+        if ((blockIdx.y & 1) != 0) return;
+        const PairDesc pb = pairs[blockIdx.y + 1];
+        for (uint64_t xx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; xx < pd.code_len;
+             xx += (uint64_t)gridDim.x * blockDim.x)
+        {
+            const int64_t x = (int64_t)xx - kPad;
+            uint32_t colA = 0, colB = 0;  // padding: zero scores
+            if (x >= 0 && x < (int64_t)pd.text_len)
+            {
+                const int tA = min(max((int)text[pd.text_off + x], 0), A - 1);
+                const int tB = min(max((int)text[pb.text_off + x], 0), A - 1);
+                for (int r = 0; r < A; ++r)
+                {
+                    colA |= ((uint32_t)table[r * A + tA] & 0xffu) << (8 * r);
+                    colB |= ((uint32_t)table[r * A + tB] & 0xffu) << (8 * r);
+                }
+            }
+            codes[pd.code_off + 2 * xx] = (int32_t)colA;
+            codes[pd.code_off + 2 * xx + 1] = (int32_t)colB;
+        }
+        return;
+    }
     for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
          x += (uint64_t)gridDim.x * blockDim.x)
     {
@@ -1424,7 +1645,10 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         d.code_off = code_bytes;
         // kArr8: code_len bytes per copy (4A copies); kArr: A arrays of code_len dwords; else one
         d.code_len = (kPad + d.text_len + 4 * kPad + 3) / 4 * 4;
-        code_bytes += pl->sk == kArr8 ? (uint64_t)A * d.code_len : pl->sk == kArr ? (uint64_t)A * d.code_len : d.code_len;
+        // (a possible pair-packed plan, decided below, needs two column profiles per column)
+        const bool maybePair = P->mode == SA_GLOBAL && R >= 16 && A <= 4;
+        code_bytes += pl->sk == kArr8 ? (uint64_t)A * d.code_len : pl->sk == kArr ? (uint64_t)A * d.code_len
+                                                                                : (maybePair ? 2 : 1) * d.code_len;
         d.out_off = outb;
         outb += d.text_len + d.pattern_len + 16;
         d.first_strip = (int32_t)pl->strips.size();
@@ -1452,11 +1676,33 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     pl->bytes_masks = mask_entries * 16;
     pl->W = choose_W(pl->pairs);
     for (const PairDesc &d : pl->pairs) pl->chain = pl->chain || d.num_strips > 1;
+    {
+        // pair-packed fill (fill_pair_kernel): global, lone strips of one shape, DNA-sized alphabet,
+        // every S + 2g in [0, 255] and every value within u16 (see process_pair)
+        bool pair = P->mode == SA_GLOBAL && !pl->chain && np >= 2 && np % 2 == 0 && A <= 4 && R >= 16 &&
+                    std::getenv("SA_NO_PAIR16") == nullptr;
+        int64_t smaxp = 0;
+        for (int e = 0; e < A * A; ++e)
+        {
+            const int64_t v = P->score_matrix[e] + off2;
+            if (v < 0 || v > 255) pair = false;
+            smaxp = std::max(smaxp, v);
+        }
+        for (int64_t p = 0; p < np && pair; ++p)
+        {
+            const PairDesc &d = pl->pairs[p];
+            if (d.text_len != pl->pairs[0].text_len || d.pattern_len != pl->pairs[0].pattern_len || d.num_strips != 1)
+                pair = false;
+            else if ((uint64_t)smaxp * std::min(d.text_len, d.pattern_len) > 65535)
+                pair = false;
+        }
+        if (pair) pl->sk = kPair;
+    }
 
     // ---- tables ----
     std::vector<int32_t> prof(4, 0), table(A * A);
     for (int e = 0; e < A * A; ++e) table[e] = (int32_t)(P->score_matrix[e] + off2);
-    if (pl->sk == kProf)
+    if (pl->sk == kProf || pl->sk == kPair)
         for (int cp = 0; cp < A; ++cp)
         {
             uint32_t w = 0;
@@ -1522,10 +1768,10 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         uint64_t nmax = 1;
         for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, d.text_len);
         const int gx = (int)std::min<uint64_t>((nmax + 255) / 256, 64);
-        for (int y0 = 0; y0 < np; y0 += 65535)
+        for (int y0 = 0; y0 < np; y0 += 65534)
         {
             // pairs beyond 65535 are handled by re-basing the pair pointer
-            const int cnt = std::min(65535, np - y0);
+            const int cnt = std::min(65534, np - y0);  // even: kPair pairs (2q, 2q+1) stay in one launch
             hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
                                pl->d_pairs + y0, pl->d_codes, pl->A, pl->sk, pl->d_table);
         }
@@ -1570,7 +1816,14 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         // chains: two workgroups of W compute waves + an I/O wave per CU; lone strips: W compute
         // waves per workgroup and up to 16 waves per CU (the batch kernel stays under 128 VGPRs)
         const int perCU = pl->chain ? std::max(1, 8 / W) : std::max(1, 16 / W);
-        const int grid = std::min(a.num_groups, std::max(1, pl->num_cu) * perCU);
+        int grid = std::min(a.num_groups, std::max(1, pl->num_cu) * perCU);
+        if (pl->sk == kPair)
+        {
+            // one wave per two strips
+            const int units = ns / 2;
+            a.num_groups = (units + W - 1) / W;
+            grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
+        }
         launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
         HIP_TRY(hipGetLastError());
         if (tlPath)

@@ -192,3 +192,27 @@ def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane):
         bad = int((got != exp).sum())
         b.close()
         assert bad == 0, (n, m, bad)
+
+
+@pytest.mark.parametrize("rows_per_lane", [16, 32])
+def test_pair_packed_fill_vs_oracle(eng, rows_per_lane):
+    """The pair-packed fill (two equal-shape global pairs per wave in u16 halves, fill_pair_kernel):
+    every pair's DIRECTION matrix, score and alignment equal the oracle's, cell by cell."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    n, m = 1500, 64 * rows_per_lane - 37
+    texts, pats = [], []
+    for k in range(4):
+        t = synthetic.random_sequence(900 + k, n, 4)
+        texts.append(t)
+        pats.append(synthetic.mutate(t, 950 + k, 4, m) if k % 2 else synthetic.random_sequence(970 + k, m, 4))
+    b = DeviceBatch(0, S, 5, texts, pats, rows_per_lane=rows_per_lane)
+    res = b.run()
+    for k in range(4):
+        got = b.directions(k)
+        exp = np.empty((m + 1) * (n + 1), np.uint8)
+        oracle.fill_only(0, texts[k], pats[k], S, 5, exp)
+        assert int((got != exp).sum()) == 0, k
+        at, ap = b.alignment(k)
+        assert dict(res[k], aligned_text=at, aligned_pattern=ap) == oracle.align(0, texts[k], pats[k], S, 5)
+    b.close()
