@@ -46,7 +46,7 @@ def main():
     stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)[0]
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     st = rows(stats)
-    fill = next(r for r in st if "fill_kernel" in r["Name"])
+    fill = next(r for r in st if "fill_kernel" in r["Name"] or "fill_pair_kernel" in r["Name"])
     avg_ns = float(fill["AverageNs"])
     bench = json.loads(open(os.path.join(src, "bench_trace.json")).read().strip().splitlines()[-1])
     wl = bench["config"]["workload"]
@@ -55,7 +55,7 @@ def main():
         cells = bench["config"]["text_len"] * bench["config"]["pattern_len"] * bench["config"]["pairs_total"] // bench["n_gpus"]
     w = counter_per_kernel(os.path.join(src, "pmc_write"), "WRITE_SIZE")
     f = counter_per_kernel(os.path.join(src, "pmc_fetch"), "FETCH_SIZE")
-    kname = next(k for k in w if "fill_kernel" in k)
+    kname = next(k for k in w if "fill_kernel" in k or "fill_pair_kernel" in k)
     wb = w[kname] * 1024.0
     fb = f.get(kname, 0.0) * 1024.0 * 2.0  # gfx950: FETCH_SIZE = half the bytes of 16-B/lane loads
     traffic = wb + fb
