@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["headline", "local", "batch"], default="headline")
+    ap.add_argument("--workload", choices=["headline", "local", "batch", "dna8k", "protein4k"], default="headline")
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -102,7 +102,24 @@ def main():
     S = synthetic.blast_matrix()
     gap = 5
     npairs = 1
-    if args.workload in ("headline", "local"):
+    if args.workload in ("dna8k", "protein4k"):
+        # BASELINE.json configs 2 and 4: DNA global 8192^2 (seeds 3/4) and protein global 4096^2 with
+        # BLOSUM50 (letters uniform over the 20 standard residues), one pair per GPU (replicas)
+        n = m = 8192 if args.workload == "dna8k" else 4096
+        A = 4 if args.workload == "dna8k" else 20
+        if A == 20:
+            mats = json.load(open(os.path.join(ROOT, "tests", "golden", "matrices.json")))
+            S = np.array(mats["blosum50"], dtype=np.int32).reshape(23, 23)
+        t = synthetic.random_sequence(3 + 1000 * rank, n, A)
+        p = synthetic.random_sequence(4 + 1000 * rank, m, A)
+        job = DeviceBatch(0, S, gap, [t], [p], device=local, rows_per_lane=args.rows_per_lane,
+                          alphabet=None if A == 4 else b"ARNDCQEGHILKMFPSTWYVBZX-")
+        cells_rank = n * m
+        pairs_rank = 1
+        workload = {"workload": f"{'dna' if A == 4 else 'protein'}_global_{n}x{m}", "pairs_per_gpu": 1,
+                    "text_len": n, "pattern_len": m, "score": "blast +5/-4" if A == 4 else "blosum50",
+                    "gap": gap, "parallelism": f"replicas{world}"}
+    elif args.workload in ("headline", "local"):
         n = m = args.size
         mode = 0 if args.workload == "headline" else 1
         t = synthetic.random_sequence(6 + 1000 * rank, n, 4)
@@ -222,6 +239,10 @@ def main():
             if args.workload == "batch":
                 # 512 pairs' worth of cells (2048 columns x 2^20 rows, one tall fill), ~2-5 s on one core
                 out["cpu_baseline"] = cpu_baseline("global", 2048, args.cpu_rows or 2048 * 512, seeds=(1000, 1001))
+            elif args.workload == "dna8k":
+                out["cpu_baseline"] = cpu_baseline("global", 8192, args.cpu_rows or 8192, seeds=(3, 4))
+            elif args.workload == "protein4k":
+                out["cpu_baseline"] = None  # the CPU sampler is DNA/blast only; see BASELINE.md §1 for protein
             else:
                 out["cpu_baseline"] = cpu_baseline("global" if args.workload == "headline" else "local",
                                                    args.size, args.cpu_rows or args.size)

@@ -147,6 +147,7 @@ struct FillArgs {
     int32_t A;
     uint32_t epoch;
     int32_t key_bits;
+    int32_t key_rowbits;        // local best-cell key: H | ~row (key_rowbits) | ~col (key_rowbits)
     uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
     uint64_t *timeline;         // debug (SA_TIMELINE): per strip {start, fed, end, hw id}, or null
     int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
@@ -525,9 +526,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                     const int row = rowTop + rho;
                     if (Hv > 0 && row <= m && c >= 1 && c <= n)
                     {
-                        const uint64_t k64 = ((uint64_t)Hv << (2 * kKeyRowBits)) |
-                                             ((kKeyMask - (uint64_t)row) << kKeyRowBits) |
-                                             (kKeyMask - (uint64_t)c);
+                        const int rb = a.key_rowbits;
+                        const uint64_t km = (1ull << rb) - 1;
+                        const uint64_t k64 = ((uint64_t)Hv << (2 * rb)) | ((km - (uint64_t)row) << rb) |
+                                             (km - (uint64_t)c);
                         lbest = max(lbest, k64);
                     }
                     best[rho] = 0;
@@ -1085,7 +1087,7 @@ struct TbArgs {
     char *out_text, *out_pattern;
     sa_result *results;
     uint64_t *timing;           // debug (SA_TB_TIMING): per pair {start, walk done, pass 1, pass 2}
-    int32_t mode, gap, A;
+    int32_t mode, gap, A, key_rowbits;
     char alphabet[33];
 };
 
@@ -1116,12 +1118,14 @@ __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
         uint64_t k = 0;
         for (int s = lane; s < pd.num_strips; s += kWave) k = max(k, a.strip_best[pd.first_strip + s]);
         k = wave_max_u64(k);
-        const int H = (int)(k >> (2 * kKeyRowBits));
+        const int rb = a.key_rowbits;
+        const uint64_t km = (1ull << rb) - 1;
+        const int H = (int)(k >> (2 * rb));
         if (H > 0)
         {
             score = H;
-            i = (int)(kKeyMask - ((k >> kKeyRowBits) & kKeyMask));
-            j = (int)(kKeyMask - (k & kKeyMask));
+            i = (int)(km - ((k >> rb) & km));
+            j = (int)(km - (k & km));
         }
         else
         {
@@ -1436,7 +1440,7 @@ int dmalloc(T **p, size_t bytes)
 
 struct sa_plan {
     int device = 0;
-    int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12;
+    int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12, key_rowbits = 21;
     int sk = 0;          // ScoreKind of the fill
     bool chain = false;  // some pair has more than one strip
     int num_cu = 0;
@@ -1586,12 +1590,13 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         sabs = std::max<int64_t>(sabs, std::llabs((long long)P->score_matrix[e]));
     }
     // numeric limits of the engine: every intermediate fits in int32, local keys fit.
-    uint64_t hmax_local = 0;
+    uint64_t hmax_local = 0, lmax = 0;
     for (int64_t p = 0; p < np; ++p)
     {
         const uint64_t n = pairs[p].text_len, m = pairs[p].pattern_len;
-        if (n >= (1u << kKeyRowBits) - 1 || m >= (1u << kKeyRowBits) - 1)
-            return fail(SA_ERR_UNSUPPORTED, "sequence longer than 2^21-2 letters");
+        if (n >= (1u << 24) - 1 || m >= (1u << 24) - 1)
+            return fail(SA_ERR_UNSUPPORTED, "sequence longer than 2^24-2 letters");
+        lmax = std::max(lmax, std::max(n, m));
         const uint64_t span = n + m;
         const uint64_t bound = ((uint64_t)sabs + (uint64_t)std::llabs(g)) * span + (uint64_t)std::llabs(g) * span;
         if (bound >= (1ull << 30)) return fail(SA_ERR_UNSUPPORTED, "scores may exceed the int32 range");
@@ -1599,8 +1604,11 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
                                   : ((uint64_t)sabs + (uint64_t)(-g)) * span;
         hmax_local = std::max(hmax_local, h);
     }
-    if (P->mode == SA_LOCAL && hmax_local >= (1ull << 22))
-        return fail(SA_ERR_UNSUPPORTED, "local scores may exceed 2^22");
+    // local best-cell keys: H | ~row | ~col in 64 bits, row / column fields sized for the longest
+    // sequence; the in-kernel block key (H << key_bits) + step must stay inside int32
+    const int key_rowbits = std::max(1, bitlen(lmax + 1));
+    if (P->mode == SA_LOCAL && (bitlen(hmax_local) > 26 || bitlen(hmax_local) > 64 - 2 * key_rowbits))
+        return fail(SA_ERR_UNSUPPORTED, "local scores may exceed the best-cell key range");
 
     sa_plan *pl = new sa_plan();
     pl->device = device;
@@ -1610,6 +1618,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     pl->R = choose_R(P, pairs, np);
     pl->U = (16 / pl->R) > 4 ? 16 / pl->R : 4;
     pl->key_bits = std::min(12, std::max(4, 30 - bitlen(hmax_local)));
+    pl->key_rowbits = key_rowbits;
     // the tables hold S + 2g (global, shifted domain) or S + g (local), see run_body
     const int64_t off2 = P->mode == SA_GLOBAL ? 2 * g : g;
     bool fits8 = true;
@@ -1798,6 +1807,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.A = pl->A;
         a.epoch = pl->epoch;
         a.key_bits = pl->key_bits;
+        a.key_rowbits = pl->key_rowbits;
         {
             const char *e = std::getenv("SA_HANDOFF_TIMEOUT_S");
             const double secs = e ? std::atof(e) : 20.0;
@@ -1869,6 +1879,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     a.mode = pl->mode;
     a.gap = pl->gap;
     a.A = pl->A;
+    a.key_rowbits = pl->key_rowbits;
     std::memcpy(a.alphabet, pl->alphabet, 33);
     // SA_TB_TIMING=<file>: debug dump of per-pair phase timestamps (s_memrealtime, 100 MHz)
     const char *tmPath = std::getenv("SA_TB_TIMING");

@@ -33,8 +33,6 @@ namespace sa {
 
 constexpr int kWave = 64;
 constexpr int kPad = 64;          // text-code padding before/after each pair
-constexpr int kKeyRowBits = 21;   // local-alignment best-cell key: H:22 | ~row:21 | ~col:21
-constexpr uint64_t kKeyMask = (1ull << kKeyRowBits) - 1;
 
 struct StripDesc {
     int32_t pair;       // owning pair
