@@ -151,6 +151,8 @@ struct FillArgs {
     uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
     uint64_t *timeline;         // debug (SA_TIMELINE): per strip {start, fed, end, hw id}, or null
     int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
+    int32_t chain_lds;          // chain launches: dynamic LDS bytes (>= group_lds_bytes(W); more
+                                // than half a CU's LDS keeps one workgroup per CU)
 };
 
 // Work unit of the fill kernel: a GROUP of W consecutive strips. A workgroup has W compute waves
@@ -169,6 +171,13 @@ __device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, 
 __device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 constexpr int kRing = 2048;        // ring entries (columns), power of two
 constexpr int kRingMask = kRing - 1;
+#ifndef SA_CODE_AHEAD
+#define SA_CODE_AHEAD 2  // R = 1 text-code loads run this many bodies ahead (1 or 2)
+#endif
+#ifndef SA_CODE_AHEAD_LOCAL
+#define SA_CODE_AHEAD_LOCAL 2
+#endif
+constexpr int kTimelineWords = 6;  // SA_TIMELINE record per strip
 constexpr int kMaxWaves = 4;       // compute waves per workgroup (+1 I/O wave: 320 threads, <= 256 VGPRs)
 
 struct GroupHdr {
@@ -440,7 +449,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     int upPrev = 0, Q = 0;
     int Fs[U];
     // text codes, double-buffered across the two bodies of a pair (no register copies)
-    int TA[NT], TB[NT];
+    // text codes: SA_CODE_AHEAD = 1 double-buffers across the two bodies of a pair; 2 keeps four
+    // buffers and loads every body's codes two bodies ahead (bodies run in quads)
+    constexpr int kAhead = R != 1 ? 1 : LOCAL ? SA_CODE_AHEAD_LOCAL : SA_CODE_AHEAD;  // taller strips: long bodies
+    int TA[NT], TB[NT], TC[NT], TD[NT];
     auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
         const int32_t *src = SK == kArr8 ? codes + s0 / 4 : codes + s0;
@@ -455,6 +467,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     };
     const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     load_codes(0, TA);
+    if constexpr (kAhead == 2) load_codes(U, TB);
     bool ok = true;
     int avail = 0;       // columns known to be in rin
     int consKnown = 0;   // columns the consumer of rout is known to have read
@@ -500,11 +513,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     consumed(U);
     prefetch(U);
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
     auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) -> bool {
         constexpr int KIND = decltype(kind)::value;
         const int s1 = s0 + U;
-        load_codes(s1, Tn);  // one body ahead
+        load_codes(s0 + kAhead * U, Tn);
         run_body<R, LOCAL, SK, KIND>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, Fs, acc);
         if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
         {
@@ -582,29 +596,62 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     // tail pairs: from the first pair holding a body with s1 > n (only where the final state is read)
     const int sTail = needFinal ? max(0, (n - 2 * U + 1 + 2 * U - 1) / (2 * U) * (2 * U)) : nSteps;
     int s0 = 0;
-    if constexpr (!kIsArr<SK>)
-        for (; ok && s0 < min(kWave, sTail); s0 += 2 * U)
-        {
-            ok = body(KStart{}, First{}, s0, TA, TB);
-            if (ok) ok = body(KStart{}, Second{}, s0 + U, TB, TA);
-        }
-    for (; ok && s0 < sTail; s0 += 2 * U)
+    if constexpr (kAhead == 2)
     {
-        ok = body(KSteady{}, First{}, s0, TA, TB);
-        if (ok) ok = body(KSteady{}, Second{}, s0 + U, TB, TA);
+        // bodies in quads up to `end` (a multiple of 2U), then at most one pair, after which the codes
+        // loaded into TC / TD move back to TA / TB (once per phase)
+        auto phase = [&](auto kind, int end) __attribute__((always_inline)) {
+            for (; ok && s0 + 2 * U < end; s0 += 4 * U)
+            {
+                ok = body(kind, First{}, s0, TA, TC);
+                if (ok) ok = body(kind, Second{}, s0 + U, TB, TD);
+                if (ok) ok = body(kind, First{}, s0 + 2 * U, TC, TA);
+                if (ok) ok = body(kind, Second{}, s0 + 3 * U, TD, TB);
+            }
+            if (ok && s0 < end)
+            {
+                ok = body(kind, First{}, s0, TA, TC);
+                if (ok) ok = body(kind, Second{}, s0 + U, TB, TD);
+                s0 += 2 * U;
+                sfor<NT>([&](auto Qc) {
+                    constexpr int q = decltype(Qc)::value;
+                    TA[q] = TC[q];
+                    TB[q] = TD[q];
+                });
+            }
+        };
+        if constexpr (!kIsArr<SK>) phase(KStart{}, min(kWave, sTail));
+        phase(KSteady{}, sTail);
+        phase(KGeneric{}, nSteps);
     }
-    for (; ok && s0 < nSteps; s0 += 2 * U)
+    else
     {
-        ok = body(KGeneric{}, First{}, s0, TA, TB);
-        if (ok) ok = body(KGeneric{}, Second{}, s0 + U, TB, TA);
+        if constexpr (!kIsArr<SK>)
+            for (; ok && s0 < min(kWave, sTail); s0 += 2 * U)
+            {
+                ok = body(KStart{}, First{}, s0, TA, TB);
+                if (ok) ok = body(KStart{}, Second{}, s0 + U, TB, TA);
+            }
+        for (; ok && s0 < sTail; s0 += 2 * U)
+        {
+            ok = body(KSteady{}, First{}, s0, TA, TB);
+            if (ok) ok = body(KSteady{}, Second{}, s0 + U, TB, TA);
+        }
+        for (; ok && s0 < nSteps; s0 += 2 * U)
+        {
+            ok = body(KGeneric{}, First{}, s0, TA, TB);
+            if (ok) ok = body(KGeneric{}, Second{}, s0 + U, TB, TA);
+        }
     }
     if (HN && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
     if (a.timeline && lane == 0)
     {
-        uint64_t *tl = a.timeline + 4 * (size_t)idx;
+        uint64_t *tl = a.timeline + kTimelineWords * (size_t)idx;
         tl[0] = tStart;
         tl[1] = tFed;
         tl[2] = __builtin_amdgcn_s_memrealtime();
+        tl[4] = cFed;  // shader clock (s_memtime): effective frequency = clocks / real time
+        tl[5] = __builtin_amdgcn_s_memtime();
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
         tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
                 (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
@@ -965,7 +1012,14 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
 template <int R, bool LOCAL, int SK>
 void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t st)
 {
-    if (chain) hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1)), group_lds_bytes(W), st, a);
+    if (chain)
+    {
+        const size_t lds = std::max(group_lds_bytes(W), (size_t)a.chain_lds);
+        if (lds > 65536)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1)), lds, st, a);
+    }
     else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
 }
 
@@ -1817,10 +1871,14 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const char *e = std::getenv("SA_IO_SLEEP");
             a.io_sleep = e ? std::max(0, std::atoi(e)) : 4;
         }
+        {
+            const char *e = std::getenv("SA_CHAIN_LDS_KB");
+            a.chain_lds = e ? std::max(0, std::atoi(e)) * 1024 : 0;
+        }
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = std::getenv("SA_TIMELINE");
         a.timeline = nullptr;
-        if (tlPath) HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * 4 * ns));
+        if (tlPath) HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * kTimelineWords * ns));
         const int W = pl->W;
         a.num_groups = (ns + W - 1) / W;
         // chains: two workgroups of W compute waves + an I/O wave per CU; lone strips: W compute
@@ -1838,7 +1896,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         HIP_TRY(hipGetLastError());
         if (tlPath)
         {
-            std::vector<uint64_t> tl(4 * (size_t)ns);
+            std::vector<uint64_t> tl(kTimelineWords * (size_t)ns);
             HIP_TRY(hipStreamSynchronize(st));
             HIP_TRY(hipMemcpy(tl.data(), a.timeline, tl.size() * 8, hipMemcpyDeviceToHost));
             HIP_TRY(hipFree(a.timeline));

@@ -216,3 +216,25 @@ def test_pair_packed_fill_vs_oracle(eng, rows_per_lane):
         at, ap = b.alignment(k)
         assert dict(res[k], aligned_text=at, aligned_pattern=ap) == oracle.align(0, texts[k], pats[k], S, 5)
     b.close()
+
+
+def test_very_long_reference_cases(eng):
+    """The reference's "very long" cases (tests/tests.cu:553-597, commented out there for run time):
+    qbpln50 (70020 x 66700 protein, gap 7) and AbHV_ORF111 (211518 x 202437 DNA, gap 5), global, vs
+    the reference's own alignSequenceCPU outputs (tests/golden/make_long.py); plus the properties:
+    the alignment re-scores to the score and the ungapped strings are the inputs."""
+    import gzip
+    import json
+    import os
+    from conftest import GOLDEN
+    with gzip.open(os.path.join(GOLDEN, "long.json.gz"), "rt") as f:
+        cases = json.load(f)
+    for case in cases:
+        A = case["A"]
+        t, p = encode(case["text"], A), encode(case["pattern"], A)
+        S = matrix(case["matrix"], A)
+        got = eng.align_pair(case["mode"], t, p, S, case["gap"])
+        assert same_result(got, case["result"]), case["name"]
+        at, ap = got["aligned_text"], got["aligned_pattern"]
+        assert _score_of(at, ap, S, case["gap"], A) == got["score"], case["name"]
+        assert at.replace("-", "") == case["text"] and ap.replace("-", "") == case["pattern"], case["name"]

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Experiment build of the engine with extra defines: tools/build_exp.sh <tag> "-DFOO=1 ..."
+# -> build_exp/libsa_<tag>.so (load it with SA_HIP_LIB=...). Development only.
+set -e
+tag=$1; shift
+root=$(cd "$(dirname "$0")/.." && pwd)
+src=$root/sequence-alignment-gpu_amd/csrc
+out=/tmp/sa_build_exp/$tag
+mkdir -p "$out"
+flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include -I$src $*"
+pids=()
+for f in sa_engine fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
+  /opt/rocm/bin/hipcc $flags -c $src/$f.hip -o $out/$f.o & pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p; done
+/opt/rocm/bin/hipcc $flags -shared $out/*.o -o $root/build_exp/libsa_$tag.so
+echo built build_exp/libsa_$tag.so

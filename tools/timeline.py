@@ -14,6 +14,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
 
 
+def max_overlap(xcc, se, cu, simd, fed, end):
+    """Largest number of strips whose [fed, end) windows overlap on one SIMD."""
+    best = 0
+    groups = {}
+    for i, k in enumerate(zip(xcc.tolist(), se.tolist(), cu.tolist(), simd.tolist())):
+        groups.setdefault(k, []).append(i)
+    for idx in groups.values():
+        ev = sorted([(int(fed[i]), 1) for i in idx] + [(int(end[i]), -1) for i in idx], key=lambda e: (e[0], e[1]))
+        cur = 0
+        for _, d in ev:
+            cur += d
+            best = max(best, cur)
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=32768)
@@ -39,7 +54,7 @@ def main():
     del os.environ["SA_TIMELINE"]
     import torch
     torch.cuda.synchronize()
-    tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 4)
+    tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 6)
     start, fed, end = (tl[:, i].astype(np.int64) for i in range(3))
     xcc = (tl[:, 3] >> 32).astype(np.int64)
     hw = (tl[:, 3] & 0xffffffff).astype(np.int64)
@@ -49,6 +64,8 @@ def main():
     nsteps = args.n + 63
     lag = np.diff(fed) * 10.0 if len(fed) > 1 else np.zeros(1)  # ns
     step_ns = (end - fed) * 10.0 / nsteps
+    clk = (tl[:, 5].astype(np.int64) - tl[:, 4].astype(np.int64))
+    mhz = clk / np.maximum(1, (end - fed)) * 100.0  # s_memtime ticks per s_memrealtime (100 MHz) tick
     W = int(os.environ.get("SA_WAVES_PER_GROUP", "4"))
     k = np.arange(1, len(fed))
     cross = (k % W) == 0
@@ -66,10 +83,15 @@ def main():
         "lag_ns_p90": round(float(np.percentile(lag, 90)), 1),
         "lag_ns_max": round(float(lag.max()), 1),
         "start_wait_ns_mean": round(float(((fed - start) * 10.0).mean()), 1),
+        "shader_mhz_mean": round(float(mhz.mean()), 1),
+        "shader_mhz_min": round(float(mhz.min()), 1),
+        "clk_per_step_mean": round(float((clk / nsteps).mean()), 1),
         "ns_per_step_by_strip": [round(float(x), 1) for x in step_ns[:: max(1, len(step_ns) // 16)]],
         "lag_ns_by_strip": [round(float(x), 1) for x in lag[:: max(1, len(lag) // 16)]],
         "xcc_of_first_16": xcc[:16].tolist(),
         "cu_se_of_first_8": [(int(c), int(s)) for c, s in zip(cu[:8], se[:8])],
+        "cus_used": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
+        "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
         "simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in hw[:8]],
     }
     print(json.dumps(rec))
