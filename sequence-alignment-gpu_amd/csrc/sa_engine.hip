@@ -82,6 +82,11 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v)
+{
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
 template <typename T>
 __device__ __forceinline__ T *uniform_ptr(T *p)
 {
@@ -174,8 +179,14 @@ constexpr int kRingMask = kRing - 1;
 #ifndef SA_CODE_AHEAD
 #define SA_CODE_AHEAD 2  // R = 1 text-code loads run this many bodies ahead (1 or 2)
 #endif
+#ifndef SA_PF_FIRST
+#define SA_PF_FIRST 1  // body boundary order: feed check, prefetch, publish, consumption word
+#endif
+#ifndef SA_ABL
+#define SA_ABL 0  // timing ablations of the hand-off (development builds only; results are wrong)
+#endif
 #ifndef SA_CODE_AHEAD_LOCAL
-#define SA_CODE_AHEAD_LOCAL 2
+#define SA_CODE_AHEAD_LOCAL 1
 #endif
 constexpr int kTimelineWords = 6;  // SA_TIMELINE record per strip
 constexpr int kMaxWaves = 4;       // compute waves per workgroup (+1 I/O wave: 320 threads, <= 256 VGPRs)
@@ -200,19 +211,20 @@ __device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int
     return !(aborted || late);
 }
 
-// Waits until the producer wave has published columns 1..need into the ring (LDS progress word).
-__device__ __forceinline__ bool wait_ring(const FillArgs &a, lds_int *prog, int need, int &avail, int lane)
+// Waits until the producer wave has published columns 1..need into the ring (LDS progress word),
+// or until the fill is aborted (timeout): the strip then runs on with whatever the ring holds and
+// the launch reports the abort, so the hot loop carries no error-path control flow.
+__device__ __forceinline__ void wait_ring(const FillArgs &a, lds_int *prog, int need, int &avail, int lane)
 {
-    if (avail >= need) return true;
     avail = uniform(lds_ld(prog));
-    if (avail >= need) return true;
+    if (avail >= need) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spin = 1;; ++spin)
     {
         __builtin_amdgcn_s_sleep(1);
         avail = uniform(lds_ld(prog));
-        if (avail >= need) return true;
-        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+        if (avail >= need) return;
+        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return;
     }
 }
 
@@ -391,8 +403,21 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
 {
     constexpr int U = Cfg<R>::U;
     constexpr int NT = Codes<R, SK>::NT;
-    const StripDesc sd = a.strips[idx];
-    const PairDesc pd = a.pairs[sd.pair];
+    // Descriptors come in through vector loads (the kernel stores to global memory, so the compiler
+    // cannot use scalar loads); making every field uniform keeps the sizes and every address derived
+    // from them in SGPRs
+    idx = uniform(idx);
+    StripDesc sd = a.strips[idx];
+    sd.pair = uniform(sd.pair);
+    sd.row0 = uniform(sd.row0);
+    sd.nsteps = uniform(sd.nsteps);
+    sd.mask_off = uniform64(sd.mask_off);
+    PairDesc pd = a.pairs[sd.pair];
+    pd.text_len = uniform64(pd.text_len);
+    pd.pattern_len = uniform64(pd.pattern_len);
+    pd.pattern_off = uniform64(pd.pattern_off);
+    pd.code_off = uniform64(pd.code_off);
+    pd.code_len = uniform64(pd.code_len);
     const int n = (int)pd.text_len, m = (int)pd.pattern_len;
     const int g = a.gap;
     const int kb = a.key_bits;
@@ -405,27 +430,27 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         c = min(max(c, 0), a.A - 1);
         prof[rho] = SK == kProf ? a.prof_tab[c] : SK == kTable ? c * a.A : c;
     });
-    // lane k at step s needs the score / code of column s-k+1: text index s - k
-    const int32_t *codes;
+    // lane k at step s needs the score / code of column s-k+1: text index s - k. Addresses are a
+    // uniform base (SGPRs) plus a 32-bit lane byte offset, so every load is one global_load with an
+    // SGPR base and one 32-bit add, without 64-bit VALU address arithmetic.
+    const char *cbase = reinterpret_cast<const char *>(a.codes + pd.code_off);
+    uint32_t coff;
     if constexpr (SK == kArr8)
-    {
         // byte copy r = k % 4 of letter a: byte kPad + x holds S[a][t[x - r]]; read from x = s0 - (k & ~3)
-        const int8_t *b8 = reinterpret_cast<const int8_t *>(a.codes + pd.code_off) +
-                           ((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3);
-        codes = reinterpret_cast<const int32_t *>(b8);
-    }
+        coff = (uint32_t)(((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
     else if constexpr (SK == kArr)
-        codes = a.codes + pd.code_off + (uint64_t)prof[0] * pd.code_len + kPad - lane;
+        coff = (uint32_t)(((uint64_t)prof[0] * pd.code_len + kPad - lane) * 4);
     else
-        codes = a.codes + pd.code_off + kPad - lane;
+        coff = (uint32_t)((kPad - lane) * 4);
     lds_int *rin = (lds_int *)(rings + w * kRing);
     lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
     lds_int *progIn = (lds_int *)&H.prog[w];
     lds_int *consIn = (lds_int *)&H.cons[w];
     lds_int *progOut = (lds_int *)&H.prog[w + 1];
     lds_int *consOut = (lds_int *)&H.cons[w + 1];
-    // this lane's first dword in the strip's direction chunks
-    uint32_t *mk = a.masks + sd.mask_off * 4 + lane * Cfg<R>::LW;
+    // the strip's direction chunks (uniform base) and this lane's byte offset in a chunk
+    uint32_t *mbase = a.masks + sd.mask_off * 4;
+    const uint32_t moff = (uint32_t)(lane * Cfg<R>::LW * 4);
     uint32_t acc[3][Cfg<R>::NW];
     sfor<Cfg<R>::NW>([&](auto Wc) {
         acc[0][decltype(Wc)::value] = 0;
@@ -455,10 +480,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     int TA[NT], TB[NT], TC[NT], TD[NT];
     auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
-        const int32_t *src = SK == kArr8 ? codes + s0 / 4 : codes + s0;
+        const uint32_t off = coff + (uint32_t)(SK == kArr8 ? s0 : s0 * 4);
         sfor<NT / 4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value * 4;
-            const i32x4u v = *(const i32x4u *)(src + q);
+            const i32x4u v = *(const i32x4u *)(cbase + off + q * 4);
             dst[q] = v.x;
             dst[q + 1] = v.y;
             dst[q + 2] = v.z;
@@ -468,54 +493,58 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     load_codes(0, TA);
     if constexpr (kAhead == 2) load_codes(U, TB);
-    bool ok = true;
     int avail = 0;       // columns known to be in rin
     int consKnown = 0;   // columns the consumer of rout is known to have read
     // The progress word and the feed values for body k+2 are read speculatively at the end of body
     // k and used at the end of body k+1 without an LDS round trip (LDS is in order per wave: values
     // read after a progress word that covers them are valid). At a body boundary the order is feed
-    // check -> publish -> consumption word -> next prefetch, so the boundary's only LDS wait (the
-    // feed check) never waits for the boundary's own writes. Feeds and publications are not masked
-    // at the ends of the text: values of columns <= 0 or > n only ever reach cells outside [1, n].
+    // check -> next prefetch -> publish -> consumption word: the only LDS wait (the feed check, one
+    // body after its reads) never waits for a boundary's writes. Feeds and publications are not
+    // masked at the ends of the text: values of columns <= 0 or > n only ever reach cells outside
+    // [1, n].
     int pfProg = 0, pfVal = 0;
     auto prefetch = [&](int base) __attribute__((always_inline)) {
-        if constexpr (HP)
+        if constexpr (HP && SA_ABL != 1)
         {
             pfProg = lds_ld(progIn);
             pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
         }
     };
     // lanes 0..U-1 of Q take the bottom values of columns base+1 .. base+U of the strip above
-    auto feed = [&](int base) __attribute__((always_inline)) -> bool {
+    auto feed = [&](int base) __attribute__((always_inline)) {
+        if constexpr (SA_ABL != 0)
+        {
+            Q = pfVal;  // timing ablation (development only): never waits, results are garbage
+            return;
+        }
         if constexpr (!HP)
         {
             // row 0 boundary. The zero is opaque on purpose: with a known-zero `old` the compiler
             // folds the up-DPP into its consumers with bound_ctrl:1, and on gfx950 wave_shr with
             // bound_ctrl does not hand lane 0 a zero (measured: wrong row 1 in strip 0)
             asm volatile("v_mov_b32 %0, 0" : "=v"(Q));
-            return true;
+            return;
         }
         const int need = min(n, base + U);
         if (__builtin_expect(uniform(pfProg) < need, 0))
         {
-            if (!wait_ring(a, progIn, need, avail, lane)) return false;
+            wait_ring(a, progIn, need, avail, lane);
             pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
         }
         Q = pfVal;  // lanes >= U: don't care
-        return true;
     };
     auto consumed = [&](int upto) __attribute__((always_inline)) {
-        if constexpr (HP)
+        if constexpr (HP && SA_ABL != 1)
             if (lane == 0) lds_st(consIn, upto);
     };
     prefetch(0);
-    ok = feed(0);
+    feed(0);
     consumed(U);
     prefetch(U);
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
-    auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) -> bool {
+    auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
         constexpr int KIND = decltype(kind)::value;
         const int s1 = s0 + U;
         load_codes(s0 + kAhead * U, Tn);
@@ -523,7 +552,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
-            store_chunk<R, LOCAL>(mk + (size_t)chunk * (kWave * Cfg<R>::LW), acc);
+            store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);
         }
         if constexpr (LOCAL)
         {
@@ -551,8 +580,15 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             }
         }
         // (after the last body this waits for the strip above's final progress word, n)
-        if (!feed(s1)) return false;
-        if constexpr (HN)
+        // The prefetched words must not be read before the body's steps: left alone, the compiler
+        // hoists the feed check (and its LDS wait) above the body, stalling right after the prefetch
+        // and asking for the strip above's values a body early.
+        if constexpr (HP) asm volatile("" : "+v"(pfProg), "+v"(pfVal) : "v"(Fs[U - 1]));
+        feed(s1);
+#if SA_PF_FIRST
+        prefetch(s1 + U);  // reads before this boundary's writes: waiting for them never waits for the writes
+#endif
+        if constexpr (HN && SA_ABL != 1)
         {
             // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
             // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
@@ -566,7 +602,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                     consKnown = uniform(lds_ld(consOut));
                     if (c0 + U - 1 - kRing <= consKnown) break;
                     __builtin_amdgcn_s_sleep(1);
-                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return false;
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
                 }
             }
             if (lane == kWave - 1)
@@ -585,8 +621,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             }
         }
         consumed(s1 + U);
+#if !SA_PF_FIRST
         prefetch(s1 + U);
-        return true;
+#endif
     };
     using KSteady = std::integral_constant<int, kSteady>;
     using KStart = std::integral_constant<int, kStart>;
@@ -601,17 +638,17 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         // bodies in quads up to `end` (a multiple of 2U), then at most one pair, after which the codes
         // loaded into TC / TD move back to TA / TB (once per phase)
         auto phase = [&](auto kind, int end) __attribute__((always_inline)) {
-            for (; ok && s0 + 2 * U < end; s0 += 4 * U)
+            for (; s0 + 2 * U < end; s0 += 4 * U)
             {
-                ok = body(kind, First{}, s0, TA, TC);
-                if (ok) ok = body(kind, Second{}, s0 + U, TB, TD);
-                if (ok) ok = body(kind, First{}, s0 + 2 * U, TC, TA);
-                if (ok) ok = body(kind, Second{}, s0 + 3 * U, TD, TB);
+                body(kind, First{}, s0, TA, TC);
+                body(kind, Second{}, s0 + U, TB, TD);
+                body(kind, First{}, s0 + 2 * U, TC, TA);
+                body(kind, Second{}, s0 + 3 * U, TD, TB);
             }
-            if (ok && s0 < end)
+            if (s0 < end)
             {
-                ok = body(kind, First{}, s0, TA, TC);
-                if (ok) ok = body(kind, Second{}, s0 + U, TB, TD);
+                body(kind, First{}, s0, TA, TC);
+                body(kind, Second{}, s0 + U, TB, TD);
                 s0 += 2 * U;
                 sfor<NT>([&](auto Qc) {
                     constexpr int q = decltype(Qc)::value;
@@ -627,20 +664,20 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     else
     {
         if constexpr (!kIsArr<SK>)
-            for (; ok && s0 < min(kWave, sTail); s0 += 2 * U)
+            for (; s0 < min(kWave, sTail); s0 += 2 * U)
             {
-                ok = body(KStart{}, First{}, s0, TA, TB);
-                if (ok) ok = body(KStart{}, Second{}, s0 + U, TB, TA);
+                body(KStart{}, First{}, s0, TA, TB);
+                body(KStart{}, Second{}, s0 + U, TB, TA);
             }
-        for (; ok && s0 < sTail; s0 += 2 * U)
+        for (; s0 < sTail; s0 += 2 * U)
         {
-            ok = body(KSteady{}, First{}, s0, TA, TB);
-            if (ok) ok = body(KSteady{}, Second{}, s0 + U, TB, TA);
+            body(KSteady{}, First{}, s0, TA, TB);
+            body(KSteady{}, Second{}, s0 + U, TB, TA);
         }
-        for (; ok && s0 < nSteps; s0 += 2 * U)
+        for (; s0 < nSteps; s0 += 2 * U)
         {
-            ok = body(KGeneric{}, First{}, s0, TA, TB);
-            if (ok) ok = body(KGeneric{}, Second{}, s0 + U, TB, TA);
+            body(KGeneric{}, First{}, s0, TA, TB);
+            body(KGeneric{}, Second{}, s0 + U, TB, TA);
         }
     }
     if (HN && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
@@ -659,9 +696,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     if constexpr (LOCAL)
     {
         const uint64_t wbest = wave_max_u64(lbest);
-        if (ok && lane == 0) a.strip_best[idx] = wbest;
+        if (lane == 0) a.strip_best[idx] = wbest;  // (after an abort the launch reports the error)
     }
-    else if (ok)
+    else
     {
         const int rm = m - sd.row0;  // strip-relative row of the last DP row
         if (rm >= 0 && rm < kWave * R && lane == rm / R)

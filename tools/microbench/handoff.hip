@@ -22,7 +22,9 @@ constexpr int U = 16;
 // V: 0 steps only; 1 + lane-63 publish (4 x ds_write_b128); 2 + lane-63 progress word;
 //    3 + consumer prefetch (2 ds_read_b32 + readfirstlane next body); 4 = 1+2+3 + cons word;
 //    5 + one ds_write_b32 by 16 lanes; 6 + 8 x ds_write_b64 by lane 63; 7 + exec-mask toggling only;
-//    8 + one taken uniform branch per body; 9 + 4 x global_load_dwordx4 (text codes) per body
+//    8 + one taken uniform branch per body; 9 + 4 x global_load_dwordx4 (text codes) per body;
+//    10 + 4 x ds_write_b128 by all lanes; 11 + 1 x ds_write_b128 by lane 63; 12 + 4 x ds_write_b32 by
+//    all lanes; 13 + readlane/writelane gather into 16 lanes + one ds_write_b32
 template <int V>
 __global__ __launch_bounds__(64) void body_kernel(const int *codes, int bodies, int *out, long long *cyc)
 {
@@ -122,6 +124,37 @@ __global__ __launch_bounds__(64) void body_kernel(const int *codes, int bodies, 
         {
             if (__builtin_amdgcn_readfirstlane(F) == 123456789) sink += 1;
         }
+        if constexpr (V == 10)
+        {
+            // 4 x ds_write_b128 by every lane (no exec mask), lane-distinct addresses
+            lds_i32x4 *dst = (lds_i32x4 *)(R + ((b * U * 4 + lane * 16) & 4095));
+            sfor<U / 4>([&](auto Xc) {
+                constexpr int x = decltype(Xc)::value;
+                dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
+            });
+        }
+        if constexpr (V == 11)
+        {
+            // one ds_write_b128 by lane 63
+            if (lane == 63) *(lds_i32x4 *)(R + ((b * U) & 2047)) = i32x4{Fs[0], Fs[5], Fs[10], Fs[15]};
+        }
+        if constexpr (V == 12)
+        {
+            // 4 x ds_write_b32 by every lane (no exec mask)
+            sfor<4>([&](auto Xc) {
+                constexpr int x = decltype(Xc)::value;
+                lds_st(R + ((b * U * 4 + x * 64 + lane) & 4095), Fs[4 * x + 3]);
+            });
+        }
+        if constexpr (V == 13)
+        {
+            // 16 x v_readlane + v_writelane gather of lane 63's values into lanes 0..15, one ds_write_b32
+            int G = 0;
+#define WL(q) { const int v = __builtin_amdgcn_readlane(Fs[q], 63); asm volatile("v_writelane_b32 %0, %1, " #q : "+v"(G) : "s"(v)); }
+            WL(0) WL(1) WL(2) WL(3) WL(4) WL(5) WL(6) WL(7) WL(8) WL(9) WL(10) WL(11) WL(12) WL(13) WL(14) WL(15)
+#undef WL
+            lds_st(R + ((b * U + lane) & 2047), G);
+        }
         sink += Fs[(b & 3)];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -153,6 +186,7 @@ int main()
     (void)hipMemset(codes, 0, 4096 * 4);
     run<0>(codes, out, cyc); run<1>(codes, out, cyc); run<2>(codes, out, cyc); run<3>(codes, out, cyc);
     run<4>(codes, out, cyc); run<5>(codes, out, cyc); run<6>(codes, out, cyc); run<7>(codes, out, cyc);
-    run<8>(codes, out, cyc); run<9>(codes, out, cyc);
+    run<8>(codes, out, cyc); run<9>(codes, out, cyc); run<10>(codes, out, cyc); run<11>(codes, out, cyc);
+    run<12>(codes, out, cyc); run<13>(codes, out, cyc);
     return 0;
 }

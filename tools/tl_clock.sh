@@ -1,10 +1,9 @@
 #!/bin/bash
-# Timeline with shader-clock stamps: effective clock, clocks per step and SIMD sharing, lone strip
-# vs full chain, with and without one chain workgroup per CU (SA_CHAIN_LDS_KB).
+# Timeline with shader-clock stamps: clocks per step and hand-off lags for growing chains.
 mkdir -p gpurun_out
 : > gpurun_out/tlc.log
-for c in "64 4 0" "256 4 0" "32768 4 0" "32768 4 96"; do set -- $c
-  echo "== m=$1 waves=$2 lds_kb=$3" >> gpurun_out/tlc.log
-  SA_CHAIN_LDS_KB=$3 timeout -k 10 60 python tools/timeline.py --n 32768 --m $1 --waves $2 >> gpurun_out/tlc.log 2>&1 || exit 1
+for m in ${MS:-64 256 1024 4096 32768}; do
+  echo "== m=$m" >> gpurun_out/tlc.log
+  timeout -k 10 60 python tools/timeline.py --n 32768 --m $m --waves 4 2>&1 | grep '^{' | python -c "import sys,json; d=json.loads(sys.stdin.read()); print({k: d[k] for k in ('total_us','ns_per_step_mean','clk_per_step_mean','lag_ns_in_group_mean','lag_ns_cross_group_mean','ns_per_step_by_strip')})" >> gpurun_out/tlc.log || exit 1
 done
-grep -v amdgpu.ids gpurun_out/tlc.log
+cat gpurun_out/tlc.log
