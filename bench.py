@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
+    ap.add_argument("--batch-chunks", type=int, default=1,
+                    help="batch: plans per rank; chunk k's traceback overlaps chunk k+1's fill")
     return ap.parse_args()
 
 
@@ -83,6 +85,51 @@ def load_traffic(workload: str):
         d = json.load(open(p))
         return d.get(workload)
     return None
+
+
+class Chunked:
+    """A rank's plans (one per chunk of its pairs). Fills run back to back on torch's current stream;
+    with more than one chunk, chunk k's traceback runs on a second stream as soon as its fill is done,
+    overlapping the next chunk's fill (the fill is HBM-bound, the traceback latency-bound)."""
+
+    def __init__(self, jobs, torch, local):
+        self.jobs, self.torch = jobs, torch
+        self.s_fill = torch.cuda.current_stream(local)
+        self.s_tb = torch.cuda.Stream(local) if len(jobs) > 1 else self.s_fill
+        self.plan = jobs[0].plan
+
+    def info(self) -> dict:
+        infos = [j.plan.info() for j in self.jobs]
+        return {"num_strips": sum(i["num_strips"] for i in infos), "rows_per_lane": infos[0]["rows_per_lane"],
+                "device_bytes": sum(i["device_bytes"] for i in infos), "mask_bytes": sum(i["mask_bytes"] for i in infos)}
+
+    def fill(self, ev=None) -> None:
+        if ev is not None:
+            ev[0].record(self.s_fill)
+        for j in self.jobs:
+            j.plan.fill(j.d_text.data_ptr(), j.d_pattern.data_ptr(), self.s_fill.cuda_stream)
+        if ev is not None:
+            ev[1].record(self.s_fill)
+
+    def fill_and_traceback(self, ev=None) -> None:
+        two = self.s_tb is not self.s_fill
+        if ev is not None:
+            ev[0].record(self.s_fill)
+        for k, j in enumerate(self.jobs):
+            j.plan.fill(j.d_text.data_ptr(), j.d_pattern.data_ptr(), self.s_fill.cuda_stream)
+            if ev is not None and k == len(self.jobs) - 1:
+                ev[1].record(self.s_fill)
+            if two:
+                self.s_tb.wait_stream(self.s_fill)
+            j.plan.traceback(self.s_tb.cuda_stream)
+        if two:
+            self.s_fill.wait_stream(self.s_tb)
+
+    def results(self) -> list[dict]:
+        out = []
+        for j in self.jobs:
+            out += j.plan.results(self.s_fill.cuda_stream)
+        return out
 
 
 def main():
@@ -135,31 +182,38 @@ def main():
         mine = distributed.shard(npairs, world, rank)
         texts = [synthetic.random_sequence(1000 + 2 * i, L, 4) for i in mine]
         pats = [synthetic.random_sequence(1001 + 2 * i, L, 4) for i in mine]
-        job = DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)
+        # even chunk sizes (the pair-packed fill takes pairs two at a time)
+        nch = max(1, min(args.batch_chunks, len(mine) // 2))
+        cuts = [len(mine) * c // nch // 2 * 2 for c in range(nch)] + [len(mine)]
+        chunks = [DeviceBatch(0, S, gap, texts[a:b], pats[a:b], device=local, rows_per_lane=args.rows_per_lane)
+                  for a, b in zip(cuts, cuts[1:]) if b > a]
+        job = Chunked(chunks, torch, local)
         cells_rank = len(mine) * L * L
         pairs_rank = len(mine)
         workload = {"workload": f"dna_global_batch_{npairs}x{L}x{L}", "pairs_total": npairs, "text_len": L,
-                    "pattern_len": L, "score": "blast +5/-4", "gap": gap, "parallelism": f"pairs_sharded{world}"}
-    info = job.plan.info()
+                    "pattern_len": L, "score": "blast +5/-4", "gap": gap, "parallelism": f"pairs_sharded{world}",
+                    "chunks_per_gpu": len(chunks)}
+    if not isinstance(job, Chunked):
+        job = Chunked([job], torch, local)
+    info = job.info()
     stream = torch.cuda.current_stream(local)
 
     dev = torch.device("cuda", local)
 
     def step(ev=None):
-        # the fill launch (the dominant kernel) is bracketed by HIP events on the stream the engine
-        # launches on (torch's current stream); the rest of a batch step is timed only by the wall clock
-        if ev is not None:
-            ev[0].record(stream)
-        job.fill()
-        if ev is not None:
-            ev[1].record(stream)
+        # the fill launches (the dominant kernel) are bracketed by HIP events on the stream the engine
+        # launches them on (torch's current stream); the rest of a batch step is timed only by the
+        # wall clock
         if args.workload == "batch":
-            # whole batch job per step: fill + traceback of this rank's pairs, results to host, and
-            # the path's exchange step — every rank's results gathered to rank 0 over RCCL (xGMI)
-            job.traceback()
+            # whole batch job per step: fill + traceback of this rank's pairs (chunk k's traceback on
+            # a second stream, overlapping chunk k+1's fill), results to host, and the path's exchange
+            # step — every rank's results gathered to rank 0 over RCCL (xGMI)
+            job.fill_and_traceback(ev)
             r = job.results()
             if world > 1:
                 distributed.gather_results(r, npairs, world, rank, dev)
+        else:
+            job.fill(ev)
 
     for _ in range(args.warmup):
         step()
@@ -181,12 +235,10 @@ def main():
     # traceback / end-to-end, outside the timed region (headline: reported only)
     torch.cuda.synchronize(local)
     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-    e0.record(stream)
-    job.fill()
-    e1.record(stream)
-    job.traceback()
+    job.fill_and_traceback((e0, e1))
     e2.record(stream)
     res = job.results()
+    # traceback: what runs after the last fill ends (with one chunk, the whole traceback)
     fill_ms_e2e, tb_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
 
     tmax = elapsed
