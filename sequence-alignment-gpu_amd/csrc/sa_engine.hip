@@ -186,7 +186,7 @@ constexpr int kRingMask = kRing - 1;
 #define SA_ABL 0  // timing ablations of the hand-off (development builds only; results are wrong)
 #endif
 #ifndef SA_CODE_AHEAD_LOCAL
-#define SA_CODE_AHEAD_LOCAL 1
+#define SA_CODE_AHEAD_LOCAL 2
 #endif
 constexpr int kTimelineWords = 6;  // SA_TIMELINE record per strip
 constexpr int kMaxWaves = 4;       // compute waves per workgroup (+1 I/O wave: 320 threads, <= 256 VGPRs)
