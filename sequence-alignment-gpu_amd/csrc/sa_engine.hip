@@ -35,90 +35,11 @@
 #include "sa_hip.h"
 #include "sa_layout.h"
 
+#include "sa_walk.h"
+#include "sa_wave.h"
+
 namespace sa {
 
-// ------------------------------------------------------------------------------------------------
-// wave-level helpers
-// ------------------------------------------------------------------------------------------------
-template <typename F, int... Is>
-__device__ __forceinline__ void sfor_impl(F &&f, std::integer_sequence<int, Is...>)
-{
-    (f(std::integral_constant<int, Is>{}), ...);
-}
-template <int N, typename F>
-__device__ __forceinline__ void sfor(F &&f)
-{
-    sfor_impl(f, std::make_integer_sequence<int, N>{});
-}
-
-// DPP lane moves (GFX9 wavefront shifts). wave_shr:1 — lane i reads lane i-1, lane 0 keeps `old`;
-// wave_shl:1 — lane i reads lane i+1, lane 63 keeps `old`; wave_rol:1 — lane i reads lane i+1 mod 64.
-__device__ __forceinline__ int dpp_shr1(int old, int src) { return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false); }
-__device__ __forceinline__ int dpp_shl1(int old, int src) { return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false); }
-__device__ __forceinline__ int dpp_rol1(int src) { return __builtin_amdgcn_update_dpp(src, src, 0x134, 0xf, 0xf, false); }
-
-// v_writelane_b32 through the LLVM intrinsic (clang exposes no builtin), so the compiler's hazard
-// recognizer sees it: a v_cmp that writes the SGPR pair needs one wait state before a v_writelane
-// reads it, which an inline-asm writelane silently violates (stale ballot bits).
-__device__ int amdgcn_writelane(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
-template <int L>
-__device__ __forceinline__ void writelane(uint32_t &acc, uint32_t v)
-{
-    acc = (uint32_t)amdgcn_writelane((int)v, L, (int)acc);
-}
-
-// Direction bits are accumulated per lane, in VGPRs: push_sign shifts a word left by one and moves
-// the sign bit of x in (v_alignbit_b32 {acc, x} >> 31), so "a > b" costs one subtraction and one
-// alignbit, with no SGPR round trip. After 32 pushes a word holds 32 consecutive (step,row) slots of
-// one plane, most recent in bit 0; a chunk of words goes to HBM as one coalesced vector store per
-// lane (sa_layout.h). All values are bounded well inside int32, so the differences
-// never overflow.
-__device__ __forceinline__ uint32_t push_sign(uint32_t acc, int x)
-{
-    return __builtin_amdgcn_alignbit(acc, (uint32_t)x, 31);
-}
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint64_t uniform64(uint64_t v)
-{
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
-           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-}
-template <typename T>
-__device__ __forceinline__ T *uniform_ptr(T *p)
-{
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
-    return (T *)(((uint64_t)hi << 32) | lo);
-}
-__device__ __forceinline__ bool all_lanes(bool p) { return ballot(p) == ballot(true); }
-
-// Maximum of a 64-bit value over the wave without divergent control flow (readlane into SGPRs).
-__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
-{
-    const int lo = (int)(uint32_t)v, hi = (int)(uint32_t)(v >> 32);
-    uint64_t best = 0;
-    for (int l = 0; l < kWave; ++l)
-    {
-        const uint64_t x = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(hi, l) << 32) |
-                           (uint32_t)__builtin_amdgcn_readlane(lo, l);
-        best = x > best ? x : best;
-    }
-    return best;
-}
-
-__device__ __forceinline__ uint64_t load_granule(const uint64_t *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_granule(uint64_t *p, uint64_t v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // ------------------------------------------------------------------------------------------------
 // fill kernel
@@ -1182,8 +1103,6 @@ struct TbArgs {
     char alphabet[33];
 };
 
-enum { kLeft = 0, kDiag = 1, kTop = 2, kStop = 3 };  // SequenceAlignment.hpp:122
-
 template <int R, int MODE>
 __global__ __launch_bounds__(64) void traceback_kernel(TbArgs a)
 {
@@ -1501,11 +1420,47 @@ int fail(int code, const std::string &msg)
         if (e_ != hipSuccess) return fail(SA_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+// Environment knobs, read once per process (the first time the engine needs one) and never again:
+// every field is a tuning or debugging switch; the defaults are the measured best settings.
+struct Knobs {
+    bool debug_sync = false;        // SA_DEBUG_SYNC: synchronise and check after every launch
+    int rows_per_lane = 0;          // SA_ROWS_PER_LANE: force R (1..32)
+    int waves_per_group = 0;        // SA_WAVES_PER_GROUP: force W (1..4)
+    bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
+    double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
+    int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
+    int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
+    const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
+    const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
+    bool tb_legacy = false;         // SA_TB_LEGACY: the step-by-step traceback kernel (A/B reference)
+    bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
+};
+
+const Knobs &knobs()
+{
+    static const Knobs k = [] {
+        Knobs v;
+        auto get = [](const char *name) -> const char * { return std::getenv(name); };
+        v.debug_sync = get("SA_DEBUG_SYNC") != nullptr;
+        if (const char *e = get("SA_ROWS_PER_LANE")) v.rows_per_lane = std::atoi(e);
+        if (const char *e = get("SA_WAVES_PER_GROUP")) v.waves_per_group = std::atoi(e);
+        v.no_pair16 = get("SA_NO_PAIR16") != nullptr;
+        if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
+        if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
+        if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
+        v.timeline = get("SA_TIMELINE");
+        v.tb_timing = get("SA_TB_TIMING");
+        v.tb_legacy = get("SA_TB_LEGACY") != nullptr;
+        v.tb_generic = get("SA_TB_GENERIC") != nullptr;
+        return v;
+    }();
+    return k;
+}
+
 // SA_DEBUG_SYNC=1: synchronise and check after every launch (names the failing kernel).
 int debug_sync(hipStream_t st, const char *what)
 {
-    static const bool on = std::getenv("SA_DEBUG_SYNC") != nullptr;
-    if (!on) return SA_OK;
+    if (!knobs().debug_sync) return SA_OK;
     hipError_t e = hipStreamSynchronize(st);
     if (e == hipSuccess) e = hipGetLastError();
     if (e != hipSuccess) return fail(SA_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
@@ -1550,6 +1505,8 @@ struct sa_plan {
     int32_t *d_score = nullptr;
     Control *d_ctrl = nullptr;
     uint8_t *d_ops = nullptr;
+    int32_t *d_rec = nullptr;  // traceback records (sa_walk.h)
+    TbHead *d_heads = nullptr;
     char *d_out_text = nullptr, *d_out_pattern = nullptr;
     sa_result *d_results = nullptr;
     const int8_t *d_text_in = nullptr, *d_pattern_in = nullptr;
@@ -1562,7 +1519,7 @@ namespace {
 int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
 {
     int R = P->rows_per_lane;
-    if (const char *e = std::getenv("SA_ROWS_PER_LANE")) R = std::atoi(e);
+    if (knobs().rows_per_lane) R = knobs().rows_per_lane;
     if (R == 1 || R == 2 || R == 4 || R == 8 || R == 16 || R == 32) return R;
     uint64_t mmax = 0;
     for (int64_t p = 0; p < np; ++p) mmax = std::max<uint64_t>(mmax, pairs[p].pattern_len);
@@ -1584,11 +1541,8 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
 // their rows off through LDS inside a group; single-strip pairs gain nothing from grouping.
 int choose_W(const std::vector<PairDesc> &pairs)
 {
-    if (const char *e = std::getenv("SA_WAVES_PER_GROUP"))
-    {
-        const int w = std::atoi(e);
-        if (w >= 1 && w <= kMaxWaves) return w;
-    }
+    const int w = knobs().waves_per_group;
+    if (w >= 1 && w <= kMaxWaves) return w;
     (void)pairs;
     return 4;
 }
@@ -1633,7 +1587,8 @@ void free_plan(sa_plan *p)
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
-                    p->d_best, p->d_score, p->d_ctrl, p->d_ops, p->d_out_text, p->d_out_pattern, p->d_results};
+                    p->d_best, p->d_score, p->d_ctrl, p->d_ops, p->d_rec, p->d_heads, p->d_out_text,
+                    p->d_out_pattern, p->d_results};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -1733,7 +1688,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
 
     // ---- layout ----
     const int R = pl->R, U = pl->U, RB = kWave * R;
-    uint64_t code_bytes = 0, mask_entries = 0, granules = 0, outb = 0;
+    uint64_t code_bytes = 0, mask_entries = 0, granules = 0, outb = 0, recw = 0;
     pl->pairs.resize(np);
     for (int64_t p = 0; p < np; ++p)
     {
@@ -1751,6 +1706,8 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
                                                                                 : (maybePair ? 2 : 1) * d.code_len;
         d.out_off = outb;
         outb += d.text_len + d.pattern_len + 16;
+        d.rec_off = recw;
+        recw += std::max(d.text_len, d.pattern_len) + 64;
         d.first_strip = (int32_t)pl->strips.size();
         const uint64_t n = d.text_len, m = d.pattern_len;
         const int ns = (n == 0 || m == 0) ? 0 : (int)((m + RB - 1) / RB);
@@ -1780,7 +1737,7 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
         // pair-packed fill (fill_pair_kernel): global, lone strips of one shape, DNA-sized alphabet,
         // every S + 2g in [0, 255] and every value within u16 (see process_pair)
         bool pair = P->mode == SA_GLOBAL && !pl->chain && np >= 2 && np % 2 == 0 && A <= 4 && R >= 16 &&
-                    std::getenv("SA_NO_PAIR16") == nullptr;
+                    !knobs().no_pair16;
         int64_t smaxp = 0;
         for (int e = 0; e < A * A; ++e)
         {
@@ -1820,12 +1777,15 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
     alloc(&pl->d_prof, sizeof(int32_t) * 4);
     alloc(&pl->d_table, sizeof(int32_t) * A * A);
     alloc(&pl->d_codes, 4 * code_bytes + 16);
-    alloc(&pl->d_masks, pl->bytes_masks + 16);
+    // (+8 KiB: the traceback's plane prefetch may read a few chunks past a strip)
+    alloc(&pl->d_masks, pl->bytes_masks + 8192);
     alloc(&pl->d_bnd, granules * 8 + 16);
     alloc(&pl->d_best, sizeof(uint64_t) * std::max<size_t>(1, pl->strips.size()));
     alloc(&pl->d_score, sizeof(int32_t) * std::max<size_t>(1, np));
     alloc(&pl->d_ctrl, sizeof(Control));
     alloc(&pl->d_ops, outb + 16);
+    alloc(&pl->d_rec, 4 * recw + 16);
+    alloc(&pl->d_heads, sizeof(TbHead) * std::max<size_t>(1, np));
     alloc(&pl->d_out_text, outb + 16);
     alloc(&pl->d_out_pattern, outb + 16);
     alloc(&pl->d_results, sizeof(sa_result) * std::max<size_t>(1, np));
@@ -1899,21 +1859,11 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.epoch = pl->epoch;
         a.key_bits = pl->key_bits;
         a.key_rowbits = pl->key_rowbits;
-        {
-            const char *e = std::getenv("SA_HANDOFF_TIMEOUT_S");
-            const double secs = e ? std::atof(e) : 20.0;
-            a.timeout_ticks = (uint64_t)(secs * 1e8);
-        }
-        {
-            const char *e = std::getenv("SA_IO_SLEEP");
-            a.io_sleep = e ? std::max(0, std::atoi(e)) : 4;
-        }
-        {
-            const char *e = std::getenv("SA_CHAIN_LDS_KB");
-            a.chain_lds = e ? std::max(0, std::atoi(e)) * 1024 : 0;
-        }
+        a.timeout_ticks = (uint64_t)(knobs().handoff_timeout_s * 1e8);
+        a.io_sleep = knobs().io_sleep;
+        a.chain_lds = knobs().chain_lds_kb * 1024;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
-        const char *tlPath = std::getenv("SA_TIMELINE");
+        const char *tlPath = knobs().timeline;
         a.timeline = nullptr;
         if (tlPath) HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * kTimelineWords * ns));
         const int W = pl->W;
@@ -1959,42 +1909,80 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     int cur = 0;
     HIP_TRY(hipGetDevice(&cur));
     HIP_TRY(hipSetDevice(pl->device));
-    TbArgs a;
-    a.text = pl->d_text_in;
-    a.pattern = pl->d_pattern_in;
-    a.strips = pl->d_strips;
-    a.pairs = pl->d_pairs;
-    a.masks = (const uint4 *)pl->d_masks;
-    a.strip_best = pl->d_best;
-    a.pair_score = pl->d_score;
-    a.ops = pl->d_ops;
-    a.out_text = pl->d_out_text;
-    a.out_pattern = pl->d_out_pattern;
-    a.results = pl->d_results;
-    a.mode = pl->mode;
-    a.gap = pl->gap;
-    a.A = pl->A;
-    a.key_rowbits = pl->key_rowbits;
-    std::memcpy(a.alphabet, pl->alphabet, 33);
+    const Knobs &kn = knobs();
     // SA_TB_TIMING=<file>: debug dump of per-pair phase timestamps (s_memrealtime, 100 MHz)
-    const char *tmPath = std::getenv("SA_TB_TIMING");
-    a.timing = nullptr;
-    if (tmPath) HIP_TRY(hipMalloc((void **)&a.timing, sizeof(uint64_t) * 4 * np));
-    launch_tb(pl->R, a, np, st);
-    HIP_TRY(hipGetLastError());
+    const char *tmPath = kn.tb_timing;
+    uint64_t *timing = nullptr;
+    if (tmPath) HIP_TRY(hipMalloc((void **)&timing, sizeof(uint64_t) * 4 * np));
+    if (!kn.tb_legacy)
+    {
+        // row / column walk (records) + expansion (sa_walk.hip)
+        WalkArgs w;
+        w.strips = pl->d_strips;
+        w.pairs = pl->d_pairs;
+        w.masks = pl->d_masks;
+        w.strip_best = pl->d_best;
+        w.pair_score = pl->d_score;
+        w.rec = pl->d_rec;
+        w.heads = pl->d_heads;
+        w.timing = timing;
+        w.gap = pl->gap;
+        w.key_rowbits = pl->key_rowbits;
+        w.fast = kn.tb_generic ? 0 : 1;
+        launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
+        HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "walk kernel")) return rc;
+        ExpandArgs x;
+        x.text = pl->d_text_in;
+        x.pattern = pl->d_pattern_in;
+        x.pairs = pl->d_pairs;
+        x.rec = pl->d_rec;
+        x.heads = pl->d_heads;
+        x.out_text = pl->d_out_text;
+        x.out_pattern = pl->d_out_pattern;
+        x.results = pl->d_results;
+        x.A = pl->A;
+        std::memcpy(x.alphabet, pl->alphabet, 33);
+        launch_expand(x, np, st);
+        HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "expand_kernel")) return rc;
+    }
+    else
+    {
+        TbArgs a;
+        a.text = pl->d_text_in;
+        a.pattern = pl->d_pattern_in;
+        a.strips = pl->d_strips;
+        a.pairs = pl->d_pairs;
+        a.masks = (const uint4 *)pl->d_masks;
+        a.strip_best = pl->d_best;
+        a.pair_score = pl->d_score;
+        a.ops = pl->d_ops;
+        a.out_text = pl->d_out_text;
+        a.out_pattern = pl->d_out_pattern;
+        a.results = pl->d_results;
+        a.mode = pl->mode;
+        a.gap = pl->gap;
+        a.A = pl->A;
+        a.key_rowbits = pl->key_rowbits;
+        std::memcpy(a.alphabet, pl->alphabet, 33);
+        a.timing = timing;
+        launch_tb(pl->R, a, np, st);
+        HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "traceback_kernel")) return rc;
+    }
     if (tmPath)
     {
         std::vector<uint64_t> tm(4 * (size_t)np);
         HIP_TRY(hipStreamSynchronize(st));
-        HIP_TRY(hipMemcpy(tm.data(), a.timing, tm.size() * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(hipFree(a.timing));
+        HIP_TRY(hipMemcpy(tm.data(), timing, tm.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(timing));
         if (FILE *f = std::fopen(tmPath, "wb"))
         {
             std::fwrite(tm.data(), 8, tm.size(), f);
             std::fclose(f);
         }
     }
-    if (int rc = debug_sync(st, "traceback_kernel")) return rc;
     HIP_TRY(hipSetDevice(cur));
     return SA_OK;
 }

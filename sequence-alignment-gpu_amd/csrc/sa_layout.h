@@ -50,6 +50,7 @@ struct PairDesc {
     uint64_t code_off;     // start of this pair's padded text-code block (R = 1: A text profiles)
     uint64_t code_len;     // dwords per code array: kPad + text_len + 4*kPad
     uint64_t out_off;      // start of this pair's output region (capacity text_len+pattern_len)
+    uint64_t rec_off;      // start of this pair's traceback records (int32, capacity max(n, m) + 64)
     int32_t first_strip, num_strips;
 };
 

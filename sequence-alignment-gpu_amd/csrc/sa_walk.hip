@@ -1,0 +1,753 @@
+// Traceback for MI355X (gfx950): scalar path walk over the direction planes + parallel letter
+// expansion. See sa_walk.h for the record format and DESIGN.md §3.2 for the measurements.
+//
+// Semantics (bit-exact with the reference CPU path):
+//   traceBackNW  alignSequenceCPU.cpp:64-114   start at (m, n); row 0 forces LEFT, column 0 TOP
+//   traceBackSW  alignSequenceCPU.cpp:10-62    start at the first maximum, stop at STOP or at the
+//                                              border (without the last index update)
+//
+// A traceback path is a staircase: inside a row it only moves LEFT, inside a column only TOP. The walk
+// therefore never steps cell by cell. It takes one scalar "find the first set bit" per ROW (row walk)
+// or per COLUMN (column walk), on WINDOWS staged in VGPRs with two bits per cell:
+//     bit 2c    the cell ends the run and the next move does not change the walk's free coordinate
+//               (row walk: TOP-only; column walk: LEFT)
+//     bit 2c+1  the cell ends the run with DIAG (local: DIAG or STOP)
+// so for a line (row / column) entered at window position u (even)
+//     p = ffs(W0[lane] >> u) = 2 * run + (1 if the leaving move is DIAG),   u += p + (p & 1)
+// is the whole line: one v_readlane (issued a line ahead), four SALU and one v_writelane of the record
+// p. Lane l of the windows is the l-th line of the current batch of 64 lines, walked from lane 63
+// down; window w covers the 16 positions after window w-1 along the free coordinate. When W0 holds
+// nothing at or after u the windows rotate (W0 <- W1 ...); after eight the kernel restages. Local
+// mode also reads STOP windows (odd bit = STOP) and ends the walk at a STOP cell. The borders are
+// encoded in the windows (global: column 0 TOP / row 0 LEFT; local: STOP), so they need no tests.
+//
+// ROW WALK (R = 1): lanes = the 64 rows of a strip (lane k = row k), windows = 8 x 16 columns left of
+//   the strip's entry column, built from the lane's own plane words (sa_layout.h: R = 1 slot e =
+//   j - 1 + k) by funnel shifts and bit interleaving. While a strip is walked, the raw planes of the
+//   strip above, around the predicted entry column, are copied to LDS by global_load_lds, so staging
+//   reads LDS, not HBM.
+// COLUMN WALK (R >= 2, the batch shapes): lanes = 64 consecutive columns (lane l = column J0 - 63 + l),
+//   windows = 8 blocks of 16 rows above the current row; a window word of lane l is gathered from the
+//   plane words of the block's strip lanes at column J0 - 63 + l (R = 32: one word = 32 rows = two
+//   blocks).
+// The 64 lines of a batch run unrolled in one asm statement (sa_walk_rows.inc, tools/gen_walk_asm.py);
+// partial batches and restages run the same logic as a C++ loop.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+#include "sa_walk.h"
+#include "sa_walk_rows.inc"
+#include "sa_wave.h"
+
+namespace sa {
+
+// Plane layout of strip height R (sa_layout.h; the fill's Cfg<R>)
+template <int R>
+struct Geo {
+    static constexpr int U = (16 / R) > 4 ? (16 / R) : 4;
+    static constexpr int CS = U * R > 32 ? U * R : 32;  // slots per chunk
+    static constexpr int NW = CS / 32;                  // words per plane per lane per chunk
+    static constexpr int LW = 2 * NW;                   // dwords per lane per chunk
+    static constexpr int RB = kWave * R;                // rows per strip
+    static constexpr int FW = R < 16 ? R : 16;          // rows one strip lane gives a 16-row block
+    static constexpr int NL = 16 / FW;                  // strip lanes per 16-row block
+};
+
+constexpr int kPfChunks = 12;  // R = 1 chunks (32 slots x 64 lanes x 2 planes = 512 B) prefetched per strip
+constexpr int kChunkDw = 128;  // dwords per R = 1 chunk
+constexpr int kPfDw = kPfChunks * kChunkDw;
+
+__device__ __forceinline__ uint32_t spread16(uint32_t x)  // bit i -> bit 2i (low 16 bits)
+{
+    x &= 0xffffu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+// Window word from 16 cells: E = bits "ends the run, free coordinate unchanged", D = "ends with DIAG
+// (local: or STOP)"; the STOP window has STOP at the odd bit.
+__device__ __forceinline__ uint32_t window(uint32_t E, uint32_t D) { return spread16(E) | (spread16(D) << 1); }
+
+// ------------------------------------------------------------------------------------------------
+// staging
+// ------------------------------------------------------------------------------------------------
+// Row walk: the eight windows of the calling lane's row (strip row = lane) for origin column jo:
+// window w, bit pair c = column jo - 16w - c. Raw plane words come from the LDS prefetch when it covers
+// every lane's chunks, else from global memory (uniform decision). sb = the strip's first dword.
+template <bool LOCAL>
+__device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const uint32_t *pf, int pfclo, int jo,
+                                         int lane, uint32_t (&W)[8], uint32_t (&S)[8])
+{
+    const int etop = jo - 1 + lane;   // slot of column jo in this lane's stream (R = 1: e = j - 1 + k)
+    const int c0 = etop >> 5;         // (arithmetic shift: etop >= -1)
+    const int b0 = 31 - (etop & 31);  // bit of slot etop in its word (a word's first slot is bit 31)
+    uint32_t r0[5], r1[5];
+    const int needLo = max(0, (jo - 1 - 128) >> 5), needHi = (jo + 62) >> 5;
+    if (pfclo != INT_MIN && needLo >= pfclo && needHi < pfclo + kPfChunks)
+    {
+        sfor<5>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            const int c = c0 - q;
+            const u32x2 v = *reinterpret_cast<const u32x2 *>(pf + max(c - pfclo, 0) * kChunkDw + lane * 2);
+            r0[q] = c >= 0 ? v.x : 0u;
+            r1[q] = c >= 0 ? v.y : 0u;
+        });
+    }
+    else
+    {
+        sfor<5>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            const int c = c0 - q;
+            const u32x2 v = *reinterpret_cast<const u32x2 *>(sb + (int64_t)max(c, 0) * kChunkDw + lane * 2);
+            r0[q] = c >= 0 ? v.x : 0u;
+            r1[q] = c >= 0 ? v.y : 0u;
+        });
+    }
+    sfor<4>([&](auto Sc) {
+        constexpr int s = decltype(Sc)::value;
+        // 32 columns jo - 32s - t (bit t): the slots continue from word c0-s into word c0-s-1
+        const uint32_t X = __builtin_amdgcn_alignbit(r0[s + 1], r0[s], b0);
+        const uint32_t Y = __builtin_amdgcn_alignbit(r1[s + 1], r1[s], b0);
+        const int z = jo - 32 * s;  // column of bit 0 (uniform): bits t < z are columns >= 1
+        const uint32_t vm = z >= 32 ? ~0u : (z <= 0 ? 0u : ((1u << z) - 1u));
+        const uint32_t c0b = (z >= 0 && z < 32) ? (1u << z) : 0u;  // column 0
+        uint32_t T, D, St = 0;
+        if constexpr (!LOCAL)
+        {
+            D = X & vm;                     // plane 0 = DIAG
+            T = (Y & ~X & vm) | c0b;        // TOP = "up > left" and not DIAG; column 0: TOP (:78-79)
+        }
+        else
+        {
+            D = (X & vm) | c0b;             // DIAG or STOP; column 0: STOP (the border ends the walk)
+            T = Y & ~X & vm;
+            St = (X & Y & vm) | c0b;
+        }
+        W[2 * s] = window(T, D);
+        W[2 * s + 1] = window(T >> 16, D >> 16);
+        if constexpr (LOCAL)
+        {
+            S[2 * s] = spread16(St) << 1;
+            S[2 * s + 1] = spread16(St >> 16) << 1;
+        }
+    });
+}
+
+// Column walk: the eight windows of the calling lane's column j = J0 - 63 + lane for the row blocks
+// G0, G0-1, ..., G0-7 (block G = pair rows 16G+1 .. 16G+16; bit pair c = row 16G + 16 - c). Block -1
+// is the row-0 border. mb = the pair's first strip's first dword.
+template <int R, bool LOCAL>
+__device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_t sstride, int J0, int G0, int lane,
+                                         uint32_t (&W)[8], uint32_t (&S)[8])
+{
+    using G_ = Geo<R>;
+    const int j = J0 - 63 + lane;
+    uint32_t f0[8], f1[8];
+    sfor<8>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        const int G = G0 - w;  // uniform
+        f0[w] = 0;
+        f1[w] = 0;
+        if (G >= 0)
+        {
+            const int r0 = 16 * G;  // first (top) row of the block, 0-based
+            const int b = r0 / G_::RB, rs = r0 - b * G_::RB;
+            const int k0 = rs / R, rho0 = rs - k0 * R;
+            const uint32_t *sb = mb + (int64_t)b * sstride;
+            sfor<G_::NL>([&](auto Tc) {
+                constexpr int t = decltype(Tc)::value;
+                const int k = k0 + t;
+                const int s = j - 1 + k;  // the strip lane's step at column j
+                const int e = max(s, 0) * R + rho0;
+                const int64_t off = (int64_t)(e / G_::CS) * (kWave * G_::LW) + k * G_::LW + (e % G_::CS) / 32;
+                const int sh = 32 - G_::FW - (e & 31);
+                constexpr uint32_t fm = G_::FW == 32 ? ~0u : ((1u << G_::FW) - 1u);
+                const uint32_t x0 = j >= 1 ? (sb[off] >> sh) & fm : 0u;
+                const uint32_t x1 = j >= 1 ? (sb[off + G_::NW] >> sh) & fm : 0u;
+                f0[w] |= x0 << (G_::FW * (G_::NL - 1 - t));
+                f1[w] |= x1 << (G_::FW * (G_::NL - 1 - t));
+            });
+        }
+    });
+    sfor<8>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        const int G = G0 - w;
+        const uint32_t x0 = f0[w], x1 = f1[w];
+        uint32_t E, D, St = 0;
+        if constexpr (!LOCAL)
+        {
+            D = x0;                                   // DIAG
+            E = ~x0 & ~x1 & 0xffffu;                  // LEFT
+            if (G == -1) E = 1;                       // row 0: LEFT to column 0 (traceBackNW :80-81)
+        }
+        else
+        {
+            D = x0;                                   // DIAG or STOP
+            E = ~x0 & ~x1 & 0xffffu;                  // LEFT
+            St = x0 & x1;
+            if (G == -1) { D = 1; E = 0; St = 1; }    // row 0: the border ends the walk
+        }
+        if (G < -1) { D = 0; E = 0; St = 0; }
+        W[w] = window(E, D);
+        if constexpr (LOCAL) S[w] = spread16(St) << 1;
+    });
+}
+
+// ------------------------------------------------------------------------------------------------
+// the walk
+// ------------------------------------------------------------------------------------------------
+// Runs the unrolled 64-line batch (lanes 63..0). Returns st: -1 = batch done, K = windows exhausted
+// at lane K, 0x100|K = STOP at lane K; lp = the last record written (or the STOP's p).
+template <bool LOCAL>
+__device__ __forceinline__ void walk_batch_asm(int &u, int &pa, int &na, int &st, int &lp, uint32_t &vrec,
+                                               uint32_t (&W)[8], uint32_t (&S)[8])
+{
+    if constexpr (!LOCAL)
+    {
+        asm volatile(SA_WALK_ROWS_GLOBAL
+                     : [u] "+s"(u), [pa] "+s"(pa), [na] "+s"(na), [st] "=&s"(st), [lp] "=&s"(lp), [rec] "+v"(vrec),
+                       [w0] "+v"(W[0]), [w1] "+v"(W[1]), [w2] "+v"(W[2]), [w3] "+v"(W[3]), [w4] "+v"(W[4]),
+                       [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7])
+                     :
+                     : "scc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",
+                       "s96", "s97");
+    }
+    else
+    {
+        asm volatile(SA_WALK_ROWS_LOCAL
+                     : [u] "+s"(u), [pa] "+s"(pa), [na] "+s"(na), [st] "=&s"(st), [lp] "=&s"(lp), [rec] "+v"(vrec),
+                       [w0] "+v"(W[0]), [w1] "+v"(W[1]), [w2] "+v"(W[2]), [w3] "+v"(W[3]), [w4] "+v"(W[4]),
+                       [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7]), [s0] "+v"(S[0]), [s1] "+v"(S[1]),
+                       [s2] "+v"(S[2]), [s3] "+v"(S[3]), [s4] "+v"(S[4]), [s5] "+v"(S[5]), [s6] "+v"(S[6]),
+                       [s7] "+v"(S[7])
+                     :
+                     : "scc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",
+                       "s96", "s97");
+    }
+}
+
+// Line walk state of one batch of 64 lines
+struct Lines {
+    int u = 0, pa = 0, na = 0;  // window position, positions skipped in this line, rotations
+    int kk = 63;                // next lane to walk
+    int lastp = 0;              // record of the last finished line
+    bool stopped = false;
+    int stopLane = 0, stopPos = 0, stopRun = 0;  // local STOP: lane, window position, run
+    uint32_t vrec = 0;
+};
+
+// The generic loop over lanes kk .. kmin (the asm's logic); `restage` refills exhausted windows.
+template <bool LOCAL, typename Restage>
+__device__ __forceinline__ void walk_lines(Lines &L, int kmin, uint32_t (&W)[8], uint32_t (&S)[8], Restage &&restage)
+{
+    while (L.kk >= kmin)
+    {
+        if (L.na > 7) restage();
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane((int)W[0], L.kk);
+        const uint64_t x = (uint64_t)w >> L.u;
+        if (x == 0)
+        {
+            L.pa += 32 - L.u;
+            L.u = 0;
+            sfor<7>([&](auto Xc) {
+                constexpr int q = decltype(Xc)::value;
+                W[q] = W[q + 1];
+                if constexpr (LOCAL) S[q] = S[q + 1];
+            });
+            W[7] = 0;
+            if constexpr (LOCAL) S[7] = 0;
+            ++L.na;
+            continue;
+        }
+        const int pp = (int)__builtin_ctz((uint32_t)x);
+        if constexpr (LOCAL)
+        {
+            const uint32_t sw = (uint32_t)__builtin_amdgcn_readlane((int)S[0], L.kk);
+            if ((sw >> (L.u + pp)) & 1u)
+            {
+                L.stopped = true;
+                L.stopLane = L.kk;
+                L.stopPos = L.u + pp;
+                L.stopRun = (L.pa + pp) >> 1;
+                return;
+            }
+        }
+        L.u += pp + (pp & 1);
+        L.vrec = (uint32_t)amdgcn_writelane(L.pa + pp, L.kk, (int)L.vrec);
+        L.lastp = L.pa + pp;
+        L.pa = 0;
+        --L.kk;
+    }
+}
+
+// The unrolled batch, then the generic loop for whatever it left (a restage or nothing).
+template <bool LOCAL, typename Restage>
+__device__ __forceinline__ void walk_batch(Lines &L, bool fast, int kmin, uint32_t (&W)[8], uint32_t (&S)[8],
+                                           Restage &&restage)
+{
+    if (fast && L.kk == 63 && kmin == 0)
+    {
+        int st, lp;
+        walk_batch_asm<LOCAL>(L.u, L.pa, L.na, st, lp, L.vrec, W, S);
+        if (st < 0)
+        {
+            L.kk = -1;
+            L.lastp = lp;
+        }
+        else
+        {
+            L.kk = st & 0xff;
+            if (LOCAL && (st & 0x100))
+            {
+                L.stopped = true;
+                L.stopLane = L.kk;
+                L.stopPos = L.u + lp;
+                L.stopRun = (L.pa + lp) >> 1;
+                return;
+            }
+        }
+    }
+    walk_lines<LOCAL>(L, kmin, W, S, restage);
+}
+
+// Start cell and score of pair p; false when there is nothing to walk (head complete).
+template <bool LOCAL>
+__device__ __forceinline__ bool walk_start(const WalkArgs &a, int p, int n, int m, int first, int nstrips, int lane,
+                                           TbHead &h, int &i, int &j)
+{
+    h.kind = kRecRows;
+    h.tail_op = kLeft;
+    h.tail = 0;
+    h.nrec = 0;
+    h.pad = 0;
+    if constexpr (!LOCAL)
+    {
+        h.score = nstrips > 0 ? a.pair_score[p] : -a.gap * (n + m);
+        i = m;
+        j = n;
+    }
+    else
+    {
+        uint64_t k = 0;
+        for (int s = lane; s < nstrips; s += kWave) k = max(k, a.strip_best[first + s]);
+        k = wave_max_u64(k);
+        const int rb = a.key_rowbits;
+        const uint64_t km = (1ull << rb) - 1;
+        const int H = (int)(k >> (2 * rb));
+        if (H > 0)
+        {
+            h.score = H;
+            i = (int)(km - ((k >> rb) & km));
+            j = (int)(km - (k & km));
+        }
+        else
+        {
+            h.score = 0;  // no positive cell: maxIJ stays 0 (alignSequenceCPU.cpp:152)
+            i = 0;
+            j = 0;
+        }
+    }
+    h.i0 = i;
+    h.j0 = j;
+    if (i > 0 && j > 0) return true;
+    // nothing to walk through: global with an empty sequence (only border moves), or local with no
+    // positive cell (empty alignment; starts (uint64)-1 are traceBackSW's initial indices)
+    if constexpr (!LOCAL)
+    {
+        h.tail = i + j;
+        h.tail_op = i > 0 ? kTop : kLeft;
+        h.start_text = h.start_pattern = (i + j) > 0 ? 0 : -1;
+    }
+    else
+    {
+        h.start_text = (int64_t)j - 1;
+        h.start_pattern = (int64_t)i - 1;
+    }
+    return false;
+}
+
+// Row walk (R = 1): one wave per pair
+template <bool LOCAL>
+__global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
+{
+    __shared__ uint32_t pfbuf[2][kPfDw];
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
+    PairDesc pd = a.pairs[p];
+    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
+    const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
+    int32_t *rec = a.rec + uniform64(pd.rec_off);
+    const uint64_t tW0 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
+    TbHead h;
+    int i, j;
+    if (walk_start<LOCAL>(a, p, n, m, first, nstrips, lane, h, i, j))
+    {
+        StripDesc sd = a.strips[first];
+        const int nsteps = uniform(sd.nsteps);
+        const uint32_t *mb = a.masks + uniform64(sd.mask_off) * 4;  // 16 B per slot
+        const int64_t sstride = (int64_t)nsteps * 4;                // dwords per strip
+        const int nchunks = nsteps >> 5;
+        int b = (i - 1) >> 6, k = (i - 1) & 63, jc = j;
+        int nrec = 0;
+        int pfb = 0, pfclo = INT_MIN;
+        Lines L;
+        // expected column drift of the path per strip (prefetch placement)
+        const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
+        while (b >= 0)
+        {
+            const uint32_t *sb = mb + (int64_t)b * sstride;
+            // this strip's prefetch has landed; the record store of the previous strip (issued
+            // after it, the youngest vector-memory operation) may still be in flight
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            uint32_t W[8], S[8];
+            int jo = jc;
+            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, S);
+            // the windows are complete before the prefetch below is issued: otherwise the wait for
+            // the staging loads (vmcnt) would also wait for the prefetch
+            asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
+            if constexpr (LOCAL)
+                asm volatile("" : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]));
+            int pfnext = INT_MIN;
+            if (b > 0)
+            {
+                // raw planes of the strip above around the predicted entry column -> LDS
+                const int pred = jc - drift;
+                const int clo = max(0, min((pred - 225) >> 5, nchunks - kPfChunks));
+                const uint32_t *src = sb - sstride + (int64_t)clo * kChunkDw;
+                sfor<kPfChunks / 2>([&](auto Xc) {
+                    constexpr int x = decltype(Xc)::value;
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void *)(src + x * 256 + lane * 4),
+                        (__attribute__((address_space(3))) void *)(&pfbuf[pfb ^ 1][x * 256]), 16, 0, 0);
+                });
+                pfnext = clo;
+            }
+            L.u = 0;
+            L.pa = 0;
+            L.na = 0;
+            L.kk = k;
+            L.vrec = 0;
+            auto restage = [&]() {
+                jo -= 16 * L.na;  // the eight windows are exhausted: the next 128 columns
+                L.na = 0;
+                L.u = 0;
+                rw_stage<LOCAL>(sb, pfbuf[pfb], INT_MIN, jo, lane, W, S);
+            };
+            walk_batch<LOCAL>(L, a.fast != 0, 0, W, S, restage);
+            // records of rows k .. kend (record index: rows walked before + k - lane)
+            const int kend = L.stopped ? L.stopLane + 1 : 0;
+            if (lane >= kend && lane <= k) rec[nrec + k - lane] = (int32_t)L.vrec;
+            nrec += k - kend + 1;
+            if (L.stopped)
+            {
+                const int iEnd = b * kWave + L.stopLane + 1;  // row of the STOP / border search
+                const int f = jo - 16 * L.na - (L.stopPos >> 1);
+                h.tail = L.stopRun;
+                if (f > 0)
+                {
+                    h.start_text = f - 1;  // a STOP cell: its indices (the loop exits before moving)
+                    h.start_pattern = iEnd - 1;
+                }
+                else
+                {
+                    // column 0 reached: the last cell before the border is (iEnd, 1) after a LEFT run,
+                    // or (iEnd + 1, 1) when the row was entered at column 0 by a DIAG
+                    h.start_text = 0;
+                    h.start_pattern = L.stopRun > 0 ? iEnd - 1 : iEnd;
+                }
+                break;
+            }
+            jc = jo - 16 * L.na - (L.u >> 1);
+            --b;
+            k = 63;
+            pfb ^= 1;
+            pfclo = pfnext;
+        }
+        h.nrec = nrec;
+        if (!L.stopped)
+        {
+            if constexpr (!LOCAL)
+            {
+                h.tail = jc;  // row 0: LEFT to column 0 (traceBackNW :80-81)
+                h.start_text = 0;
+                h.start_pattern = 0;
+            }
+            else
+            {
+                // row 0 reached from row 1, whose leaving cell is column jc + DIAG
+                h.start_text = jc + (L.lastp & 1) - 1;
+                h.start_pattern = 0;
+            }
+        }
+    }
+    if (lane == 0)
+    {
+        a.heads[p] = h;
+        if (a.timing)
+        {
+            a.timing[2 * (size_t)p] = tW0;
+            a.timing[2 * (size_t)p + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
+// Column walk (R >= 2): one wave per pair
+template <int R, bool LOCAL>
+__global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
+{
+    const int p = blockIdx.x;
+    const int lane = threadIdx.x;
+    PairDesc pd = a.pairs[p];
+    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
+    const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
+    int32_t *rec = a.rec + uniform64(pd.rec_off);
+    const uint64_t tW0 = a.timing ? __builtin_amdgcn_s_memrealtime() : 0;
+    TbHead h;
+    int i, j;
+    if (walk_start<LOCAL>(a, p, n, m, first, nstrips, lane, h, i, j))
+    {
+        h.kind = kRecCols;
+        h.tail_op = kTop;
+        StripDesc sd = a.strips[first];
+        const int nsteps = uniform(sd.nsteps);
+        const uint32_t *mb = a.masks + uniform64(sd.mask_off) * 4;
+        const int64_t sstride = (int64_t)nsteps * R * 4;  // dwords per strip (nsteps * R slots of 16 B)
+        int G0 = (i - 1) >> 4;                            // block of the current row
+        int J0 = j;                                       // lane 63 = column J0
+        int nrec = 0;
+        Lines L;
+        L.u = 2 * (16 * G0 + 16 - i);
+        while (J0 >= 1)
+        {
+            uint32_t W[8], S[8];
+            cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W, S);
+            const int kmin = max(0, 64 - J0);  // lanes of columns >= 1
+            L.pa = 0;
+            L.na = 0;
+            L.kk = 63;
+            L.vrec = 0;
+            auto restage = [&]() {
+                G0 -= L.na;  // the eight blocks are exhausted: the next eight above
+                L.na = 0;
+                L.u = 0;
+                cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W, S);
+            };
+            walk_batch<LOCAL>(L, a.fast != 0, kmin, W, S, restage);
+            const int kend = L.stopped ? L.stopLane + 1 : kmin;
+            if (lane >= kend) rec[nrec + 63 - lane] = (int32_t)L.vrec;
+            nrec += 64 - kend;
+            G0 -= L.na;
+            if (L.stopped)
+            {
+                const int jEnd = J0 - 63 + L.stopLane;           // column of the STOP / border search
+                const int f = 16 * G0 + 16 - (L.stopPos >> 1);   // row of the found cell
+                h.tail = L.stopRun;
+                if (f > 0)
+                {
+                    h.start_text = jEnd - 1;  // a STOP cell
+                    h.start_pattern = f - 1;
+                }
+                else
+                {
+                    // row 0 reached: the last cell before the border is (1, jEnd) after a TOP run, or
+                    // (1, jEnd + 1) when the column was entered at row 0 by a DIAG
+                    h.start_text = L.stopRun > 0 ? jEnd - 1 : jEnd;
+                    h.start_pattern = 0;
+                }
+                break;
+            }
+            J0 -= 64;
+        }
+        h.nrec = nrec;
+        if (!L.stopped)
+        {
+            const int icur = 16 * G0 + 16 - (L.u >> 1);  // row after the move into column 0 (0: row 0)
+            if constexpr (!LOCAL)
+            {
+                h.tail = icur;  // column 0: TOP to row 0 (traceBackNW :78-79)
+                h.start_text = 0;
+                h.start_pattern = 0;
+            }
+            else
+            {
+                // column 0 reached from column 1, whose leaving cell is row icur + DIAG
+                h.start_text = 0;
+                h.start_pattern = icur + (L.lastp & 1) - 1;
+            }
+        }
+    }
+    if (lane == 0)
+    {
+        a.heads[p] = h;
+        if (a.timing)
+        {
+            a.timing[2 * (size_t)p] = tW0;
+            a.timing[2 * (size_t)p + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// expansion: records -> aligned strings (forward order) and the per-pair result
+// ------------------------------------------------------------------------------------------------
+constexpr int kExpThreads = 256;
+
+__device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *lds, int64_t &total)
+{
+    const int t = threadIdx.x;
+    lds[t] = v;
+    __syncthreads();
+    for (int d = 1; d < kExpThreads; d <<= 1)
+    {
+        const int64_t x = t >= d ? lds[t - d] : 0;
+        __syncthreads();
+        lds[t] += x;
+        __syncthreads();
+    }
+    total = lds[kExpThreads - 1];
+    const int64_t incl = lds[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
+{
+    __shared__ int64_t scan[kExpThreads];
+    __shared__ char alpha[40];
+    const int p = blockIdx.x;
+    const int t = threadIdx.x;
+    if (t < 33) alpha[t] = a.alphabet[t];
+    const TbHead h = a.heads[p];
+    const PairDesc pd = a.pairs[p];
+    const int32_t *rec = a.rec + pd.rec_off;
+    const int8_t *tx = a.text + pd.text_off;
+    const int8_t *px = a.pattern + pd.pattern_off;
+    char *ot = a.out_text + pd.out_off;
+    char *op = a.out_pattern + pd.out_off;
+    const int N = h.nrec;
+    const int per = (N + kExpThreads - 1) / kExpThreads;
+    const int lo = min(N, t * per), hi = min(N, lo + per);
+    // pass 1: ops and letters consumed along the walk's free coordinate, this thread's records
+    int64_t cnt = 0, cons = 0;
+    for (int q = lo; q < hi; ++q)
+    {
+        const int v = rec[q];
+        cnt += (v >> 1) + 1;
+        cons += (v >> 1) + (v & 1);
+    }
+    int64_t tot;  // both sums in one 64-bit scan (each < 2^31)
+    const int64_t ex = block_exclusive_scan((cnt << 32) | cons, scan, tot);
+    const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
+    const int64_t totCnt = tot >> 32, totCons = tot & 0xffffffffll;
+    const int64_t L = totCnt + h.tail;
+    const char GAP = alpha[a.A];
+    // pass 2
+    int64_t P = P0;
+    if (h.kind == kRecRows)
+    {
+        // record q: row i0 - q entered at column j; `run` LEFTs, then DIAG (to column j - run - 1) or TOP
+        int64_t i = (int64_t)h.i0 - lo, j = (int64_t)h.j0 - C0;
+        for (int q = lo; q < hi; ++q)
+        {
+            const int v = rec[q];
+            const int run = v >> 1, d = v & 1;
+            const int64_t flo = L - 1 - P - run;  // forward position of the leaving move
+            const int64_t jl = j - run;           // column of the leaving cell
+            ot[flo] = d ? alpha[tx[jl - 1]] : GAP;
+            op[flo] = alpha[px[i - 1]];
+            for (int r = 0; r < run; ++r)
+            {
+                ot[flo + 1 + r] = alpha[tx[jl + r]];
+                op[flo + 1 + r] = GAP;
+            }
+            P += run + 1;
+            j = jl - d;
+            i -= 1;
+        }
+    }
+    else
+    {
+        // record q: column j0 - q entered at row i; `run` TOPs, then DIAG (to row i - run - 1) or LEFT
+        int64_t j = (int64_t)h.j0 - lo, i = (int64_t)h.i0 - C0;
+        for (int q = lo; q < hi; ++q)
+        {
+            const int v = rec[q];
+            const int run = v >> 1, d = v & 1;
+            const int64_t flo = L - 1 - P - run;
+            const int64_t il = i - run;  // row of the leaving cell
+            ot[flo] = alpha[tx[j - 1]];
+            op[flo] = d ? alpha[px[il - 1]] : GAP;
+            for (int r = 0; r < run; ++r)
+            {
+                ot[flo + 1 + r] = GAP;
+                op[flo + 1 + r] = alpha[px[il + r]];
+            }
+            P += run + 1;
+            i = il - d;
+            j -= 1;
+        }
+    }
+    // the trailing run: forward positions 0 .. tail-1, ending at the walk's last cell
+    {
+        const int64_t iT = h.kind == kRecRows ? (int64_t)h.i0 - N : (int64_t)h.i0 - totCons;
+        const int64_t jT = h.kind == kRecRows ? (int64_t)h.j0 - totCons : (int64_t)h.j0 - N;
+        for (int64_t f = t; f < h.tail; f += kExpThreads)
+        {
+            if (h.tail_op == kLeft)
+            {
+                ot[f] = alpha[tx[jT - h.tail + f]];
+                op[f] = GAP;
+            }
+            else
+            {
+                ot[f] = GAP;
+                op[f] = alpha[px[iT - h.tail + f]];
+            }
+        }
+    }
+    if (t == 0)
+    {
+        sa_result r;
+        r.score = h.score;
+        r.status = SA_OK;
+        r.num_alignment_bytes = (uint64_t)L;
+        r.start_text = (uint64_t)h.start_text;
+        r.start_pattern = (uint64_t)h.start_pattern;
+        a.results[p] = r;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launches
+// ------------------------------------------------------------------------------------------------
+template <bool LOCAL>
+void launch_walk_m(int R, const WalkArgs &a, int np, hipStream_t st)
+{
+    switch (R)
+    {
+    case 1: hipLaunchKernelGGL(walk_rw_kernel<LOCAL>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((walk_cw_kernel<2, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((walk_cw_kernel<4, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((walk_cw_kernel<8, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 16: hipLaunchKernelGGL((walk_cw_kernel<16, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    default: hipLaunchKernelGGL((walk_cw_kernel<32, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    }
+}
+
+void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
+{
+    if (local) launch_walk_m<true>(R, a, np, st);
+    else launch_walk_m<false>(R, a, np, st);
+}
+
+void launch_expand(const ExpandArgs &a, int np, hipStream_t st)
+{
+    hipLaunchKernelGGL(expand_kernel, dim3(np), dim3(kExpThreads), 0, st, a);
+}
+
+}  // namespace sa
