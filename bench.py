@@ -32,6 +32,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 
+# BASELINE.json's metric for the headline; the other workloads are its configs 2-5, labelled as such
+METRICS = {
+    "headline": "GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA NW",
+    "local": "GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA SW (config 3)",
+    "batch": "GCUPS (DP cell updates/s), 4096 x 2048^2 DNA NW batch, fill + traceback (config 5)",
+    "dna8k": "GCUPS (DP cell updates/s), 8k x 8k DNA NW (config 2)",
+    "protein4k": "GCUPS (DP cell updates/s), 4k x 4k protein NW, BLOSUM50 (config 4)",
+}
+_DNA = "synthetic (splitmix64 i.i.d. DNA, blast +5/-4, gap 5)"
+DATA = {"headline": _DNA, "local": _DNA, "batch": _DNA, "dna8k": _DNA,
+        "protein4k": "synthetic (splitmix64 i.i.d. protein, letters 0..19 of the 23-letter alphabet, BLOSUM50, gap 5)"}
+
 
 def parse():
     ap = argparse.ArgumentParser()
@@ -48,18 +60,29 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(mode: str, n: int, rows: int, seeds=(6, 7)) -> dict:
+def _matrix_file(S: np.ndarray) -> str:
+    """The score matrix as the reference's whitespace-separated text file (utilities.cpp:117-148)."""
+    with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
+        for row in np.asarray(S, dtype=np.int64):
+            f.write(" ".join(str(int(v)) for v in row) + "\n")
+        return f.name
+
+
+def cpu_baseline(mode: str, n: int, rows: int, seeds=(6, 7), S=None, letters: int = 4,
+                 label: str = "DNA blast") -> dict:
     """Single-core CPU fill on a bounded sample of the same workload, on this host. Prefers the
     reference's own CPU code (oracle/_ref/ref_align, built from /root/reference), else the oracle port."""
+    from sa_amd import synthetic
+    S = synthetic.blast_matrix() if S is None else np.asarray(S, dtype=np.int32)
+    A = S.shape[0]
     ref = os.path.join(ROOT, "oracle", "_ref", "ref_align")
     cells = rows * n
     if os.path.exists(ref):
-        with tempfile.NamedTemporaryFile("w", suffix=".txt", delete=False) as f:
-            f.write("5 -4 -4 -4\n-4 5 -4 -4\n-4 -4 5 -4\n-4 -4 -4 5\n")
-            mat = f.name
+        mat = _matrix_file(S)
         try:
             out = subprocess.run([ref, "fillbench", mode, str(rows + 1), str(n + 1), str(seeds[0]), str(seeds[1]),
-                                  "4", "5", mat, "1"], capture_output=True, text=True, check=True, timeout=600)
+                                  str(A), "5", mat, "1", str(letters)], capture_output=True, text=True, check=True,
+                                 timeout=600)
             us = json.loads(out.stdout.strip().splitlines()[-1])["us"]
         finally:
             os.unlink(mat)
@@ -67,16 +90,15 @@ def cpu_baseline(mode: str, n: int, rows: int, seeds=(6, 7)) -> dict:
     else:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
-        from sa_amd import synthetic
-        t = synthetic.random_sequence(seeds[0], n, 4)
-        p = synthetic.random_sequence(seeds[1], rows, 4)
+        t = synthetic.random_sequence(seeds[0], n, letters)
+        p = synthetic.random_sequence(seeds[1], rows, letters)
         M = np.empty((rows + 1) * (n + 1), np.uint8)
         t0 = time.perf_counter()
-        oracle.fill_only(0 if mode == "global" else 1, t, p, synthetic.blast_matrix(), 5, M)
+        oracle.fill_only(0 if mode == "global" else 1, t, p, S, 5, M)
         us = (time.perf_counter() - t0) * 1e6
         kind = "port"
     return {"value": round(cells / us / 1e3, 4), "unit": "GCUPS", "cores": 1, "kind": kind,
-            "sample": f"{mode} fill {rows}x{n} DNA blast gap 5 (same synthetic stream), 1 thread, "
+            "sample": f"{mode} fill {rows}x{n} {label} gap 5 (same synthetic stream), 1 thread, "
                       f"{us / 1e6:.2f} s"}
 
 
@@ -295,7 +317,7 @@ def main():
         tr = load_traffic(workload["workload"])
         traffic = tr["bytes_per_launch"] if tr else None
         out = {
-            "metric": "GCUPS (DP cell updates/s) + achieved HBM GB/s, 32k x 32k DNA NW",
+            "metric": METRICS[args.workload],
             "value": round(value, 3),
             "unit": "GCUPS",
             "n_gpus": world,
@@ -306,7 +328,7 @@ def main():
             "scaling": "weak" if args.workload != "batch" else "strong",
             "vs_baseline": None,
             "dtype": "int32",
-            "data": "synthetic (splitmix64 i.i.d. DNA, blast +5/-4, gap 5)",
+            "data": DATA[args.workload],
             "config": dict(workload, rows_per_lane=info["rows_per_lane"], strips_per_gpu=info["num_strips"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -335,7 +357,8 @@ def main():
             elif args.workload == "dna8k":
                 out["cpu_baseline"] = cpu_baseline("global", 8192, args.cpu_rows or 8192, seeds=(3, 4))
             elif args.workload == "protein4k":
-                out["cpu_baseline"] = None  # the CPU sampler is DNA/blast only; see BASELINE.md §1 for protein
+                out["cpu_baseline"] = cpu_baseline("global", 4096, args.cpu_rows or 4096, seeds=(3, 4), S=S,
+                                                   letters=20, label="protein BLOSUM50 (letters 0..19 of 23)")
             else:
                 out["cpu_baseline"] = cpu_baseline("global" if args.workload == "headline" else "local",
                                                    args.size, args.cpu_rows or args.size)

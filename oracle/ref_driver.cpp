@@ -11,8 +11,10 @@
 // Modes
 //   ref_align cli <alignSequence args...>   -> exactly what mainDriver.cu:4-27 prints for the CPU device
 //   ref_align batch <in.bin> <out.bin>       -> alignSequenceCPU on binary records (format below)
-//   ref_align fillbench <global|local> <rows> <cols> <seedT> <seedP> <A> <gap> <matrixfile> <reps>
-//                                            -> best-of-reps fill time in microseconds (benchmarks.cu:102-187)
+//   ref_align fillbench <global|local> <rows> <cols> <seedT> <seedP> <A> <gap> <matrixfile> <reps> [letters]
+//                                            -> best-of-reps fill time in microseconds (benchmarks.cu:102-187);
+//                                               letters (default A) = how many letter codes the synthetic
+//                                               stream draws from (20 for protein: the standard residues)
 //   ref_align parse <alignSequence args...>  -> dumps the Request parseArguments builds (encoded bytes)
 //
 // batch record (little endian):  int32 mode(0=global,1=local), int32 A, int32 gap, int32 pad,
@@ -125,12 +127,13 @@ static int runFillBench(int argc, const char *argv[])
     request.gapPenalty = std::stoi(argv[8]);
     parseScoreMatrixFile(argv[9], A, request.scoreMatrix);
     const int reps = std::stoi(argv[10]);
+    const int letters = argc > 11 ? std::stoi(argv[11]) : A;
     request.textNumBytes = numCols - 1;
     request.patternNumBytes = numRows - 1;
     request.textBytes = new char[numCols - 1];
     request.patternBytes = new char[numRows - 1];
-    for (uint64_t i = 0; i + 1 < numCols; ++i) request.textBytes[i] = char((splitmix64(seedT) >> 33) % A);
-    for (uint64_t i = 0; i + 1 < numRows; ++i) request.patternBytes[i] = char((splitmix64(seedP) >> 33) % A);
+    for (uint64_t i = 0; i + 1 < numCols; ++i) request.textBytes[i] = char((splitmix64(seedT) >> 33) % letters);
+    for (uint64_t i = 0; i + 1 < numRows; ++i) request.patternBytes[i] = char((splitmix64(seedP) >> 33) % letters);
     std::vector<char> M(numRows * numCols);
     double best = 1e300;
     int score = 0;
