@@ -82,6 +82,11 @@ int sa_align_pair(const sa_params *params, const char *text, uint64_t text_len,
                   const char *pattern, uint64_t pattern_len, int device, sa_result *out,
                   char *aligned_text, char *aligned_pattern, uint64_t cap, double *fill_us);
 
+/* sa_align_pair keeps, per device, a stream, two events and a grow-only device arena across calls
+ * (calls on one device are serialised). This releases them for `device` (-1: every device); they
+ * are also released at process exit. */
+int sa_release_workspace(int device);
+
 /* ---- plans: many pairs, device-resident inputs, explicit stream ------------------------- */
 
 /* Build a plan (strip layout, workspace) for num_pairs pairs on `device`. Allocates all device

@@ -1,0 +1,970 @@
+// MI355X (gfx950 / CDNA4) DP fill kernels: Needleman-Wunsch / Smith-Waterman direction planes.
+//
+// Replaces the reference's GPU path (robertszafa/sequence-alignment-gpu alignSequenceGPU.cu:73-653)
+// with a new design; see DESIGN.md and sa_layout.h for the data layout. Semantics follow the
+// reference CPU path (alignSequenceCPU.cpp), bit-exact:
+//   cell recurrence and tie rule      alignSequenceCPU.cpp:175-190 (local), :259-273 (global)
+//   boundaries                        :145-149, :163-164 (local), :232-236, :247-248 (global)
+//   local best cell (first max)       :191-192
+//   tracebacks                        traceBackNW :64-114, traceBackSW :10-62
+//
+// Fill kernel (one wave64 per strip; workgroups of W strips + an I/O wave; dynamic group queue):
+//   * lane k owns R rows and works on column s-k+1 at step s; the value from the row above
+//     arrives by a DPP wave_shr:1 lane shift, lane 0 is fed from the strip above through an LDS
+//     ring (inside a workgroup) or epoch-tagged global granules moved by the I/O wave;
+//   * the substitution score comes from a per-row profile register (DNA: four int8 scores packed
+//     in one VGPR, selected by v_bfe_i32 on the text code) or from an LDS table (protein);
+//   * global alignment runs in the shifted domain F = H + g*(i+j), where the recurrence
+//     becomes F = max(Fdiag + s + 2g, Fleft, Fup) and every boundary is 0;
+//   * the direction of each cell is two bits pushed into per-lane VGPR words (one subtraction and
+//     one v_alignbit per bit, no SGPR round trip); every 32 (step,row) slots a lane's words go to
+//     HBM in one coalesced vector store per wave.
+//
+// Compiled once per strip height R: fill_r<R>.hip defines SA_FILL_R and includes this file.
+#ifndef SA_FILL_R
+#error "sa_fill.hip is compiled through fill_r<R>.hip (SA_FILL_R = strip rows per lane)"
+#endif
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+
+#include "sa_fill.h"
+#include "sa_wave.h"
+
+namespace sa {
+
+// ------------------------------------------------------------------------------------------------
+// fill kernel
+// ------------------------------------------------------------------------------------------------
+template <int R>
+struct Cfg {
+    static constexpr int U = (16 / R) > 4 ? (16 / R) : 4;  // steps per unrolled body
+    static constexpr int SB = U * R;                        // (step,row) slots per body
+    static constexpr int CS = SB > 32 ? SB : 32;            // slots per stored chunk (sa_layout.h)
+    static constexpr int NW = CS / 32;                      // words per plane per lane per chunk
+    static constexpr int LW = 2 * NW;                       // dwords per lane per chunk (2 planes)
+    static constexpr int BPC = CS / SB;                     // bodies per chunk (1 or 2)
+    static_assert(SB % 16 == 0 && (CS % SB) == 0, "bodies must tile chunks");
+};
+
+// Work unit of the fill kernel: a GROUP of W consecutive strips. A workgroup has W compute waves
+// (one strip each) and one I/O wave. Compute waves only ever exchange rows through LDS rings:
+// ring[w] feeds compute wave w; wave w writes its bottom row into ring[w+1]. The I/O wave links the
+// group to its neighbours in global memory: it copies the previous group's granules into ring[0]
+// and drains ring[W] into granules for the next group. Keeping every global store and poll out of
+// the compute waves matters: on gfx9 a store shares the vmcnt counter with the text-code loads, and
+// a cross-XCD (sc1) store takes ~0.7 us to retire, which would stall the next load wait.
+typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, never flat
+// Ring and progress-word accesses are relaxed workgroup-scope atomics: the compiler keeps them in
+// program order and re-reads them every time, without the s_waitcnt lgkmcnt(0) it puts after every
+// volatile access.
+// LDS executes one wave's ds operations in order, which is the only ordering the rings rely on.
+__device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+constexpr int kRing = 2048;        // ring entries (columns), power of two
+constexpr int kRingMask = kRing - 1;
+#ifndef SA_CODE_AHEAD
+#define SA_CODE_AHEAD 2  // R = 1 text-code loads run this many bodies ahead (1 or 2)
+#endif
+#ifndef SA_PF_FIRST
+#define SA_PF_FIRST 1  // body boundary order: feed check, prefetch, publish, consumption word
+#endif
+#ifndef SA_ABL
+#define SA_ABL 0  // timing ablations of the hand-off (development builds only; results are wrong)
+#endif
+#ifndef SA_CODE_AHEAD_LOCAL
+#define SA_CODE_AHEAD_LOCAL 2
+#endif
+
+struct GroupHdr {
+    int S[32 * 32];                // generic score table (A <= 32)
+    int prog[kMaxWaves + 1];       // prog[w]: columns published into ring[w]
+    int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
+    int group;                     // group index taken from the queue
+    int pad[1];
+};
+__host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + (size_t)(W + 1) * kRing * 4; }
+
+// Bounded-spin helper, called every few polls: false (and the abort word raised) after the
+// timeout, or as soon as another wave has given up.
+__device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int lane)
+{
+    // 100 MHz constant clock
+    const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+    if (late && lane == 0) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int aborted = uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return !(aborted || late);
+}
+
+// Waits until the producer wave has published columns 1..need into the ring (LDS progress word),
+// or until the fill is aborted (timeout): the strip then runs on with whatever the ring holds and
+// the launch reports the abort, so the hot loop carries no error-path control flow.
+__device__ __forceinline__ void wait_ring(const FillArgs &a, lds_int *prog, int need, int &avail, int lane)
+{
+    avail = uniform(lds_ld(prog));
+    if (avail >= need) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 1;; ++spin)
+    {
+        __builtin_amdgcn_s_sleep(1);
+        avail = uniform(lds_ld(prog));
+        if (avail >= need) return;
+        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return;
+    }
+}
+
+// Ring slot of column c (1-based) in every LDS ring. The +14 puts the first column of a producer
+// body's bottom-row values (c = s0 - 62, s0 a multiple of U) on a slot that is a multiple of U, so
+// lane 63 publishes a body with U/4 ds_write_b128 that never straddle the ring's end.
+__device__ __forceinline__ int ring_slot(int c) { return (c + 14) & kRingMask; }
+static_assert(kRing % 16 == 0, "ring must hold whole bodies");
+
+
+// a + sign_extend(byte B of w), one VALU op
+template <int B>
+__device__ __forceinline__ int add_sbyte(int a, int w)
+{
+    int r;
+    if constexpr (B == 0) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(a), "v"(w));
+    else if constexpr (B == 1) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(a), "v"(w));
+    else if constexpr (B == 2) asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(a), "v"(w));
+    else asm("v_add_u32_sdwa %0, %1, sext(%2) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(a), "v"(w));
+    return r;
+}
+
+// Text-code dwords per body: one per step, or one per four steps (kArr8).
+template <int R, int SK>
+struct Codes {
+    static constexpr int NT = SK == kArr8 ? Cfg<R>::U / 4 : Cfg<R>::U;
+};
+
+// One unrolled body of U steps. Body kinds (KIND):
+//   kSteady  every lane is on a column >= 1. Lanes past column n compute garbage, which is harmless:
+//            it only ever flows to lanes that are past n as well, their direction planes are never
+//            read, their bottom-row values are never read and their local best-cell keys are
+//            filtered by column; only the global score and the local best-cell keys need the exact
+//            final state (kGeneric).
+//   kStart   the first bodies (s < 63, kProf / kTable only): lane k is still left of column 1 while
+//            s < k. Forcing the substitution score of those virtual cells to 0 keeps their state at
+//            the boundary value (see the recurrences), so lane k enters column 1 with exactly the
+//            column-0 state. Text profiles need no kStart bodies: their padding scores are 0.
+//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row, and
+//            local strips' last bodies).
+enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
+// Recurrences (per lane-row; diag/up/left are the neighbours' values):
+//   global, shifted domain F = H + g(i+j): F = max(Fdiag + S + 2g, Fleft, Fup), boundaries 0;
+//     DIAG iff Fdiag + S + 2g > max(Fleft, Fup); plane 1 = raw "up > left".
+//   local, H with the gap folded into the score: X = max(Hdiag + S + g, max(Hleft, Hup)),
+//     H = max(X - g, 0) (one saturating subtraction: X >= 0); DIAG iff Hdiag + S + g > max(Hleft,
+//     Hup) (the reference's D > max(L, U) with every candidate shifted by +g); raw TOP iff Hup >
+//     Hleft; STOP iff H == 0 (alignSequenceCPU.cpp:175-190).
+// Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
+// wave_shr:1 whose `old` operand is this step's feed register Q (lane 0 keeps Q's lane 0 = the
+// strip above's bottom value for this column); Q is dead afterwards, so the DPP writes in place. The
+// next step's feed register is Q shifted down one lane (wave_shl:1, bound_ctrl), computed first.
+// The strip's bottom row (F[R-1] of lane 63 after each step) is not moved at all: every step's F[R-1]
+// stays in its own register Fs[q] until the body ends, when lane 63 publishes all U of them.
+template <int R, bool LOCAL, int SK, int KIND>
+__device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
+                                         int kb, const int (&prof)[R], const int (&T)[Codes<R, SK>::NT],
+                                         int (&F)[R], int (&best)[R], int &upPrev, int Q,
+                                         int (&Fs)[Cfg<R>::U], uint32_t (&acc)[3][Cfg<R>::NW])
+{
+    constexpr int U = Cfg<R>::U;
+    sfor<U>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int s = s0 + q;
+        const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
+        int up = dpp_shr1(Q, F[R - 1]);
+        Q = Qn;
+        int diag = upPrev;
+        upPrev = up;
+        constexpr bool RAMP = KIND == kGeneric;
+        bool act = true;
+        if constexpr (RAMP)
+        {
+            const int c = s - lane;
+            act = (c >= 0) && (c < n);
+        }
+        const bool real = KIND != kStart || lane <= s;  // kStart: column s-lane+1 >= 1
+        const int kmask = (1 << kb) - 1;
+        const int Ks = kmask - (s & kmask);  // local: later column in a block = smaller key
+        sfor<R>([&](auto Rc) {
+            constexpr int rho = decltype(Rc)::value;
+            constexpr int w = ((q * R + rho) / 32) % Cfg<R>::NW;
+            int D;
+            if constexpr (SK == kArr8) D = add_sbyte<q & 3>(diag, T[q >> 2]);
+            else
+            {
+                int sc;
+                if constexpr (SK == kArr) sc = T[q];
+                else if constexpr (SK == kProf) sc = __builtin_amdgcn_sbfe(prof[rho], T[q], 8);
+                else sc = ldsS[prof[rho] + T[q]];
+                if constexpr (KIND == kStart) sc = real ? sc : 0;
+                D = diag + sc;
+            }
+            const int left = F[rho];
+            const int M = max(left, up);
+            acc[0][w] = push_sign(acc[0][w], M - D);      // DIAG
+            acc[1][w] = push_sign(acc[1][w], left - up);  // raw "up > left" (global) / raw TOP (local)
+            int Fn;
+            if constexpr (!LOCAL)
+            {
+                Fn = max(D, M);
+            }
+            else
+            {
+                const unsigned X = (unsigned)max(D, M);
+                Fn = (int)__builtin_elementwise_sub_sat(X, (unsigned)g);
+                acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
+                const int key = (Fn << kb) + Ks;
+                if constexpr (RAMP) best[rho] = act ? max(best[rho], key) : best[rho];
+                else best[rho] = max(best[rho], key);
+            }
+            if constexpr (RAMP) Fn = act ? Fn : left;
+            diag = left;
+            up = Fn;
+            F[rho] = Fn;
+        });
+        Fs[q] = F[R - 1];
+    });
+}
+
+// Stores one finished chunk: lane k's LW dwords at chunk*64*LW + k*LW (one coalesced wave store).
+template <int R, bool LOCAL>
+__device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)[3][Cfg<R>::NW])
+{
+    constexpr int NW = Cfg<R>::NW;
+    uint32_t v[2 * NW];
+    sfor<NW>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        if constexpr (LOCAL)
+        {
+            const uint32_t d = acc[0][w], t = acc[1][w], z = acc[2][w];
+            v[w] = d | z;
+            v[NW + w] = (t & ~d) | z;
+        }
+        else
+        {
+            v[w] = acc[0][w];
+            v[NW + w] = acc[1][w];
+        }
+    });
+    if constexpr (NW == 1)
+    {
+        *reinterpret_cast<u32x2 *>(dst) = u32x2{v[0], v[1]};
+    }
+    else
+    {
+        sfor<NW / 2>([&](auto Xc) {
+            constexpr int x = decltype(Xc)::value;
+            *reinterpret_cast<u32x4 *>(dst + 4 * x) = u32x4{v[4 * x], v[4 * x + 1], v[4 * x + 2], v[4 * x + 3]};
+        });
+    }
+}
+
+// One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
+// compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
+// codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
+// kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
+template <int R, bool LOCAL, int SK, bool HP, bool HN>
+__device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
+{
+    constexpr int U = Cfg<R>::U;
+    constexpr int NT = Codes<R, SK>::NT;
+    // Descriptors come in through vector loads (the kernel stores to global memory, so the compiler
+    // cannot use scalar loads); making every field uniform keeps the sizes and every address derived
+    // from them in SGPRs
+    idx = uniform(idx);
+    StripDesc sd = a.strips[idx];
+    sd.pair = uniform(sd.pair);
+    sd.row0 = uniform(sd.row0);
+    sd.nsteps = uniform(sd.nsteps);
+    sd.mask_off = uniform64(sd.mask_off);
+    PairDesc pd = a.pairs[sd.pair];
+    pd.text_len = uniform64(pd.text_len);
+    pd.pattern_len = uniform64(pd.pattern_len);
+    pd.pattern_off = uniform64(pd.pattern_off);
+    pd.code_off = uniform64(pd.code_off);
+    pd.code_len = uniform64(pd.code_len);
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
+    const int g = a.gap;
+    const int kb = a.key_bits;
+    const int rowTop = sd.row0 + lane * R;
+    int prof[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        const int i = rowTop + rho;
+        int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
+        c = min(max(c, 0), a.A - 1);
+        prof[rho] = SK == kProf ? a.prof_tab[c] : SK == kTable ? c * a.A : c;
+    });
+    // lane k at step s needs the score / code of column s-k+1: text index s - k. Addresses are a
+    // uniform base (SGPRs) plus a 32-bit lane byte offset, so every load is one global_load with an
+    // SGPR base and one 32-bit add, without 64-bit VALU address arithmetic.
+    const char *cbase = reinterpret_cast<const char *>(a.codes + pd.code_off);
+    uint32_t coff;
+    if constexpr (SK == kArr8)
+        // byte copy r = k % 4 of letter a: byte kPad + x holds S[a][t[x - r]]; read from x = s0 - (k & ~3)
+        coff = (uint32_t)(((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+    else if constexpr (SK == kArr)
+        coff = (uint32_t)(((uint64_t)prof[0] * pd.code_len + kPad - lane) * 4);
+    else
+        coff = (uint32_t)((kPad - lane) * 4);
+    lds_int *rin = (lds_int *)(rings + w * kRing);
+    lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
+    lds_int *progIn = (lds_int *)&H.prog[w];
+    lds_int *consIn = (lds_int *)&H.cons[w];
+    lds_int *progOut = (lds_int *)&H.prog[w + 1];
+    lds_int *consOut = (lds_int *)&H.cons[w + 1];
+    // the strip's direction chunks (uniform base) and this lane's byte offset in a chunk
+    uint32_t *mbase = a.masks + sd.mask_off * 4;
+    const uint32_t moff = (uint32_t)(lane * Cfg<R>::LW * 4);
+    uint32_t acc[3][Cfg<R>::NW];
+    sfor<Cfg<R>::NW>([&](auto Wc) {
+        acc[0][decltype(Wc)::value] = 0;
+        acc[1][decltype(Wc)::value] = 0;
+        acc[2][decltype(Wc)::value] = 0;
+    });
+    const int nSteps = sd.nsteps;  // a multiple of 2U
+    // Lanes must stop at column n (kGeneric bodies at the end) where the final state is read: the
+    // global score H(m, n) in the strip holding row m, and the local best-cell keys (a garbage key
+    // past column n could shadow a real one of the same key block). Other strips run their tail
+    // unmasked.
+    const bool needFinal = LOCAL || (m - sd.row0 >= 0 && m - sd.row0 < kWave * R);
+
+    // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
+    int F[R], best[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        F[rho] = 0;
+        best[rho] = 0;
+    });
+    int upPrev = 0, Q = 0;
+    int Fs[U];
+    // text codes, double-buffered across the two bodies of a pair (no register copies)
+    // text codes: SA_CODE_AHEAD = 1 double-buffers across the two bodies of a pair; 2 keeps four
+    // buffers and loads every body's codes two bodies ahead (bodies run in quads)
+    constexpr int kAhead = R != 1 ? 1 : LOCAL ? SA_CODE_AHEAD_LOCAL : SA_CODE_AHEAD;  // taller strips: long bodies
+    int TA[NT], TB[NT], TC[NT], TD[NT];
+    auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
+        typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+        const uint32_t off = coff + (uint32_t)(SK == kArr8 ? s0 : s0 * 4);
+        sfor<NT / 4>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value * 4;
+            const i32x4u v = *(const i32x4u *)(cbase + off + q * 4);
+            dst[q] = v.x;
+            dst[q + 1] = v.y;
+            dst[q + 2] = v.z;
+            dst[q + 3] = v.w;
+        });
+    };
+    const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    load_codes(0, TA);
+    if constexpr (kAhead == 2) load_codes(U, TB);
+    int avail = 0;       // columns known to be in rin
+    int consKnown = 0;   // columns the consumer of rout is known to have read
+    // The progress word and the feed values for body k+2 are read speculatively at the end of body
+    // k and used at the end of body k+1 without an LDS round trip (LDS is in order per wave: values
+    // read after a progress word that covers them are valid). At a body boundary the order is feed
+    // check -> next prefetch -> publish -> consumption word: the only LDS wait (the feed check, one
+    // body after its reads) never waits for a boundary's writes. Feeds and publications are not
+    // masked at the ends of the text: values of columns <= 0 or > n only ever reach cells outside
+    // [1, n].
+    int pfProg = 0, pfVal = 0;
+    auto prefetch = [&](int base) __attribute__((always_inline)) {
+        if constexpr (HP && SA_ABL != 1)
+        {
+            pfProg = lds_ld(progIn);
+            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
+        }
+    };
+    // lanes 0..U-1 of Q take the bottom values of columns base+1 .. base+U of the strip above
+    auto feed = [&](int base) __attribute__((always_inline)) {
+        if constexpr (SA_ABL != 0)
+        {
+            Q = pfVal;  // timing ablation (development only): never waits, results are garbage
+            return;
+        }
+        if constexpr (!HP)
+        {
+            // row 0 boundary. The zero is opaque on purpose: with a known-zero `old` the compiler
+            // folds the up-DPP into its consumers with bound_ctrl:1, and on gfx950 wave_shr with
+            // bound_ctrl does not hand lane 0 a zero (measured: wrong row 1 in strip 0)
+            asm volatile("v_mov_b32 %0, 0" : "=v"(Q));
+            return;
+        }
+        const int need = min(n, base + U);
+        if (__builtin_expect(uniform(pfProg) < need, 0))
+        {
+            wait_ring(a, progIn, need, avail, lane);
+            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
+        }
+        Q = pfVal;  // lanes >= U: don't care
+    };
+    auto consumed = [&](int upto) __attribute__((always_inline)) {
+        if constexpr (HP && SA_ABL != 1)
+            if (lane == 0) lds_st(consIn, upto);
+    };
+    prefetch(0);
+    feed(0);
+    consumed(U);
+    prefetch(U);
+    const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
+    uint64_t lbest = 0;
+    auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
+        constexpr int KIND = decltype(kind)::value;
+        const int s1 = s0 + U;
+        load_codes(s0 + kAhead * U, Tn);
+        run_body<R, LOCAL, SK, KIND>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, Fs, acc);
+        if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
+        {
+            const int chunk = (s1 * R) / Cfg<R>::CS - 1;
+            store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);
+        }
+        if constexpr (LOCAL)
+        {
+            const int kmask = (1 << kb) - 1;
+            if (((s1 & kmask) == 0) || s1 >= nSteps)
+            {
+                const int blockBase = s0 & ~kmask;
+                sfor<R>([&](auto Rc) {
+                    constexpr int rho = decltype(Rc)::value;
+                    const int key = best[rho];
+                    const int Hv = key >> kb;
+                    const int st = blockBase + (kmask - (key & kmask));
+                    const int c = st - lane + 1;
+                    const int row = rowTop + rho;
+                    if (Hv > 0 && row <= m && c >= 1 && c <= n)
+                    {
+                        const int rb = a.key_rowbits;
+                        const uint64_t km = (1ull << rb) - 1;
+                        const uint64_t k64 = ((uint64_t)Hv << (2 * rb)) | ((km - (uint64_t)row) << rb) |
+                                             (km - (uint64_t)c);
+                        lbest = max(lbest, k64);
+                    }
+                    best[rho] = 0;
+                });
+            }
+        }
+        // (after the last body this waits for the strip above's final progress word, n)
+        // The prefetched words must not be read before the body's steps: left alone, the compiler
+        // hoists the feed check (and its LDS wait) above the body, stalling right after the prefetch
+        // and asking for the strip above's values a body early.
+        if constexpr (HP) asm volatile("" : "+v"(pfProg), "+v"(pfVal) : "v"(Fs[U - 1]));
+        feed(s1);
+#if SA_PF_FIRST
+        prefetch(s1 + U);  // reads before this boundary's writes: waiting for them never waits for the writes
+#endif
+        if constexpr (HN && SA_ABL != 1)
+        {
+            // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
+            // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
+            const int c0 = s0 - (kWave - 2);
+            const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
+            if (__builtin_expect(c0 + U - 1 - kRing > consKnown, 0))
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    consKnown = uniform(lds_ld(consOut));
+                    if (c0 + U - 1 - kRing <= consKnown) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+                }
+            }
+            if (lane == kWave - 1)
+            {
+                typedef int i32x4 __attribute__((ext_vector_type(4)));
+                typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
+                lds_i32x4 *dst = (lds_i32x4 *)(rout + ring_slot(c0));
+                sfor<U / 4>([&](auto Xc) {
+                    constexpr int x = decltype(Xc)::value;
+                    dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
+                });
+                // the values go before the progress word: a compiler-only fence (LDS executes one
+                // wave's operations in order)
+                asm volatile("" ::: "memory");
+                lds_st(progOut, top);
+            }
+        }
+        consumed(s1 + U);
+#if !SA_PF_FIRST
+        prefetch(s1 + U);
+#endif
+    };
+    using KSteady = std::integral_constant<int, kSteady>;
+    using KStart = std::integral_constant<int, kStart>;
+    using KGeneric = std::integral_constant<int, kGeneric>;
+    using First = std::false_type;
+    using Second = std::true_type;
+    // tail pairs: from the first pair holding a body with s1 > n (only where the final state is read)
+    const int sTail = needFinal ? max(0, (n - 2 * U + 1 + 2 * U - 1) / (2 * U) * (2 * U)) : nSteps;
+    int s0 = 0;
+    if constexpr (kAhead == 2)
+    {
+        // bodies in quads up to `end` (a multiple of 2U), then at most one pair, after which the codes
+        // loaded into TC / TD move back to TA / TB (once per phase)
+        auto phase = [&](auto kind, int end) __attribute__((always_inline)) {
+            for (; s0 + 2 * U < end; s0 += 4 * U)
+            {
+                body(kind, First{}, s0, TA, TC);
+                body(kind, Second{}, s0 + U, TB, TD);
+                body(kind, First{}, s0 + 2 * U, TC, TA);
+                body(kind, Second{}, s0 + 3 * U, TD, TB);
+            }
+            if (s0 < end)
+            {
+                body(kind, First{}, s0, TA, TC);
+                body(kind, Second{}, s0 + U, TB, TD);
+                s0 += 2 * U;
+                sfor<NT>([&](auto Qc) {
+                    constexpr int q = decltype(Qc)::value;
+                    TA[q] = TC[q];
+                    TB[q] = TD[q];
+                });
+            }
+        };
+        if constexpr (!kIsArr<SK>) phase(KStart{}, min(kWave, sTail));
+        phase(KSteady{}, sTail);
+        phase(KGeneric{}, nSteps);
+    }
+    else
+    {
+        if constexpr (!kIsArr<SK>)
+            for (; s0 < min(kWave, sTail); s0 += 2 * U)
+            {
+                body(KStart{}, First{}, s0, TA, TB);
+                body(KStart{}, Second{}, s0 + U, TB, TA);
+            }
+        for (; s0 < sTail; s0 += 2 * U)
+        {
+            body(KSteady{}, First{}, s0, TA, TB);
+            body(KSteady{}, Second{}, s0 + U, TB, TA);
+        }
+        for (; s0 < nSteps; s0 += 2 * U)
+        {
+            body(KGeneric{}, First{}, s0, TA, TB);
+            body(KGeneric{}, Second{}, s0 + U, TB, TA);
+        }
+    }
+    if (HN && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
+    if (a.timeline && lane == 0)
+    {
+        uint64_t *tl = a.timeline + kTimelineWords * (size_t)idx;
+        tl[0] = tStart;
+        tl[1] = tFed;
+        tl[2] = __builtin_amdgcn_s_memrealtime();
+        tl[4] = cFed;  // shader clock (s_memtime): effective frequency = clocks / real time
+        tl[5] = __builtin_amdgcn_s_memtime();
+        // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
+        tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+    }
+    if constexpr (LOCAL)
+    {
+        const uint64_t wbest = wave_max_u64(lbest);
+        if (lane == 0) a.strip_best[idx] = wbest;  // (after an abort the launch reports the error)
+    }
+    else
+    {
+        const int rm = m - sd.row0;  // strip-relative row of the last DP row
+        if (rm >= 0 && rm < kWave * R && lane == rm / R)
+        {
+            int v = F[0];
+            sfor<R>([&](auto Rc) {
+                constexpr int rho = decltype(Rc)::value;
+                if (rho == rm % R) v = F[rho];
+            });
+            a.pair_score[sd.pair] = v - g * (m + n);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// pair-packed fill (global mode, lone strips, DNA-sized alphabets): two independent pairs of the same
+// shape in the two 16-bit halves of every register
+// ------------------------------------------------------------------------------------------------
+// The shifted-domain global recurrence only needs unsigned add / max and sign bits of differences,
+// so when every value fits u16 (0 <= S + 2g <= 255, (max S + 2g) * min(m, n) <= 65535: F is
+// non-negative and bounded by that) and every difference compared fits i16 (|M - D|, |left - up| <=
+// 2 (max S + 2g)), one v_pk_* instruction advances both pairs.
+//   * Scores: per text column the code block holds two "column profiles" {colA, colB}, byte r of
+//     colA = S[r][tA] + 2g (zero in the padding); each row keeps one fixed selector
+//     rA | 0x0c00 | (4 + rB) << 16 | 0x0c000000, and one v_perm_b32(colB, colA, sel) gives the row's
+//     two scores as u16 halves.
+//   * Direction bits: slot σ of a 16-slot group sits at bit 15 - σ of each half. Slots s and s+8
+//     (s < 8) are rows ρ and ρ+8 of the same step (R >= 16); one v_perm_b32 gathers the four sign
+//     bits (both pairs, both slots) onto byte MSBs (bits 15, 7, 31, 23), one shift by s moves them to
+//     15-s, 7-s, 31-s, 23-s, and one v_and_or_b32 inserts them: 3 VALU per 4 bits.
+//   * At the body's end v_perm_b32 splits the packed words back into each pair's ordinary 32-slot
+//     words, so the stored planes, the traceback and the decoders are exactly those of the unpacked
+//     kernel.
+// About 4.5 VALU per cell instead of 8.2.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as16(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+template <int R>
+__device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane)
+{
+    constexpr int U = Cfg<R>::U;
+    constexpr int SB = Cfg<R>::SB;      // slots per body (per pair)
+    constexpr int NP = SB / 16;         // packed words per plane per body
+    constexpr int NW = Cfg<R>::NW, LW = Cfg<R>::LW;
+    static_assert(R >= 16 && Cfg<R>::BPC == 1 && SB % 32 == 0, "pair kernel: R >= 16, a body is one chunk");
+    const StripDesc dA = a.strips[sA], dB = a.strips[sA + 1];
+    const PairDesc pA = a.pairs[dA.pair], pB = a.pairs[dB.pair];
+    const int n = (int)pA.text_len, m = (int)pA.pattern_len;
+    const int g = a.gap;
+    const int rowTop = 1 + lane * R;
+    uint32_t rsel[R];
+    sfor<R>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        const int i = rowTop + rho;
+        const int cA = i <= m ? min(max((int)a.pattern[pA.pattern_off + i - 1], 0), a.A - 1) : 0;
+        const int cB = i <= m ? min(max((int)a.pattern[pB.pattern_off + i - 1], 0), a.A - 1) : 0;
+        rsel[rho] = (uint32_t)cA | 0x0c00u | ((uint32_t)(4 + cB) << 16) | 0x0c000000u;
+    });
+    // column profiles {colA, colB} per column, in pair A's code block (2 dwords per column)
+    const int32_t *codes = a.codes + pA.code_off + 2 * (kPad - lane);
+    uint32_t *mkA = a.masks + dA.mask_off * 4 + lane * LW;
+    uint32_t *mkB = a.masks + dB.mask_off * 4 + lane * LW;
+    const int nSteps = dA.nsteps;
+    uint32_t F[R];
+    sfor<R>([&](auto Rc) { F[decltype(Rc)::value] = 0; });
+    uint32_t upPrev = 0;
+    int Q;
+    int TA[2 * U], TB[2 * U];
+    auto load_codes = [&](int s0, int (&dst)[2 * U]) __attribute__((always_inline)) {
+        typedef int i32x4u __attribute__((ext_vector_type(4), aligned(8)));
+        sfor<U / 2>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value * 4;
+            const i32x4u v = *(const i32x4u *)(codes + 2 * s0 + q);
+            dst[q] = v.x;
+            dst[q + 1] = v.y;
+            dst[q + 2] = v.z;
+            dst[q + 3] = v.w;
+        });
+    };
+    load_codes(0, TA);
+    auto body = [&](auto kind, int s0, int (&T)[2 * U], int (&Tn)[2 * U]) __attribute__((always_inline)) {
+        constexpr bool RAMP = decltype(kind)::value;  // tail: lanes outside [1, n] keep their state
+        const int s1 = s0 + U;
+        load_codes(s1, Tn);
+        uint32_t acc[2][NP];
+        asm volatile("v_mov_b32 %0, 0" : "=v"(Q));  // row 0 boundary (opaque zero: see feed())
+        sfor<U>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
+            uint32_t up = (uint32_t)dpp_shr1(Q, (int)F[R - 1]);
+            Q = Qn;
+            uint32_t diag = upPrev;
+            upPrev = up;
+            bool act = true;
+            if constexpr (RAMP)
+            {
+                const int c = s0 + q - lane;
+                act = (c >= 0) && (c < n);
+            }
+            const uint32_t colA = (uint32_t)T[2 * q], colB = (uint32_t)T[2 * q + 1];
+            uint32_t x0[R], x1[R];
+            sfor<R>([&](auto Rc) {
+                constexpr int rho = decltype(Rc)::value;
+                const uint32_t sc = __builtin_amdgcn_perm(colB, colA, rsel[rho]);
+                const u16x2 D = as16(diag) + as16(sc);
+                const uint32_t left = F[rho];
+                const u16x2 M = __builtin_elementwise_max(as16(left), as16(up));
+                uint32_t Fn = as32(__builtin_elementwise_max(D, M));
+                x0[rho] = as32(M - D);                     // DIAG iff sign
+                x1[rho] = as32(as16(left) - as16(up));     // up > left iff sign
+                if constexpr (RAMP) Fn = act ? Fn : left;
+                diag = left;
+                up = Fn;
+                F[rho] = Fn;
+                // rows rho-8 and rho of a 16-row group are slots s and s+8 of packed word w: insert
+                // as soon as both exist (keeps at most 8 rows of differences live)
+                if constexpr (rho % 16 >= 8)
+                {
+                    constexpr int sl = rho % 16 - 8;
+                    constexpr int w = (q * R + rho) / 16;
+                    constexpr uint32_t mask = (0x80808080u >> sl);
+                    const uint32_t y0 = __builtin_amdgcn_perm(x0[rho - 8], x0[rho], 0x07030501u) >> sl;
+                    const uint32_t y1 = __builtin_amdgcn_perm(x1[rho - 8], x1[rho], 0x07030501u) >> sl;
+                    if constexpr (sl == 0)
+                    {
+                        acc[0][w] = y0 & mask;
+                        acc[1][w] = y1 & mask;
+                    }
+                    else
+                    {
+                        acc[0][w] |= y0 & mask;
+                        acc[1][w] |= y1 & mask;
+                    }
+                }
+            });
+        });
+        // split the packed words into each pair's 32-slot words: {plane 0 words, plane 1 words}
+        const int chunk = (s1 * R) / Cfg<R>::CS - 1;
+        uint32_t vA[LW], vB[LW];
+        sfor<NW>([&](auto Wc) {
+            constexpr int w = decltype(Wc)::value;
+            sfor<2>([&](auto Pc) {
+                constexpr int p = decltype(Pc)::value;
+                vA[p * NW + w] = __builtin_amdgcn_perm(acc[p][2 * w], acc[p][2 * w + 1], 0x05040100u);
+                vB[p * NW + w] = __builtin_amdgcn_perm(acc[p][2 * w], acc[p][2 * w + 1], 0x07060302u);
+            });
+        });
+        uint32_t *dA_ = mkA + (size_t)chunk * (kWave * LW);
+        uint32_t *dB_ = mkB + (size_t)chunk * (kWave * LW);
+        sfor<LW / 4>([&](auto Xc) {
+            constexpr int x = decltype(Xc)::value;
+            *reinterpret_cast<u32x4 *>(dA_ + 4 * x) = u32x4{vA[4 * x], vA[4 * x + 1], vA[4 * x + 2], vA[4 * x + 3]};
+            *reinterpret_cast<u32x4 *>(dB_ + 4 * x) = u32x4{vB[4 * x], vB[4 * x + 1], vB[4 * x + 2], vB[4 * x + 3]};
+        });
+    };
+    // tail pairs of bodies from the first pair holding a body with s1 > n (the global score row is
+    // in every lone strip)
+    const int sTail = max(0, n / (2 * U) * (2 * U));
+    int s0 = 0;
+    for (; s0 < sTail; s0 += 2 * U)
+    {
+        body(std::false_type{}, s0, TA, TB);
+        body(std::false_type{}, s0 + U, TB, TA);
+    }
+    for (; s0 < nSteps; s0 += 2 * U)
+    {
+        body(std::true_type{}, s0, TA, TB);
+        body(std::true_type{}, s0 + U, TB, TA);
+    }
+    const int rm = m - 1;  // strip-relative row of the last DP row
+    if (lane == rm / R)
+    {
+        uint32_t v = F[0];
+        sfor<R>([&](auto Rc) {
+            constexpr int rho = decltype(Rc)::value;
+            if (rho == rm % R) v = F[rho];
+        });
+        a.pair_score[dA.pair] = (int)(v & 0xffffu) - g * (m + n);
+        a.pair_score[dB.pair] = (int)(v >> 16) - g * (m + n);
+    }
+}
+
+// One wave per two strips (pairs sA, sA+1); 4 waves per workgroup; dynamic queue over strip pairs.
+template <int R>
+__global__ __launch_bounds__(kWave * kMaxWaves, 2) void fill_pair_kernel(FillArgs a)
+{
+    __shared__ int unit;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = uniform((int)(threadIdx.x / kWave));
+    const int W = (int)(blockDim.x / kWave);
+    const int units = a.num_strips / 2;
+    while (true)
+    {
+        __syncthreads();
+        if (threadIdx.x == 0) unit = (int)atomicAdd(&a.ctrl->queue_head, 1u);
+        __syncthreads();
+        const int grp = uniform(unit);
+        if (grp * W >= units) break;
+        const int u = grp * W + w;
+        if (u < units) process_pair<R>(a, 2 * u, lane);
+    }
+}
+
+// The I/O wave of a group: global granules of the previous group's last strip -> ring[0], and
+// ring[W'] (W' = compute waves with a strip) -> granules for the next group. Only lane 0 polls the
+// granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
+// load the fabric the running strips use); the bytes move 64 columns per instruction.
+__device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
+{
+    const int first = grp * W;
+    const int last = min(first + W, a.num_strips) - 1;
+    const StripDesc sf = a.strips[first];
+    const StripDesc sl = a.strips[last];
+    const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
+    const int nOut = (sl.flags & kHasNext) ? (int)a.pairs[sl.pair].text_len : 0;
+    if (nIn == 0 && nOut == 0) return;
+    const int wl = last - first + 1;  // ring fed by the last strip
+    lds_int *r0 = (lds_int *)rings;
+    lds_int *prog0 = (lds_int *)&H.prog[0];
+    lds_int *cons0 = (lds_int *)&H.cons[0];
+    lds_int *rl = (lds_int *)(rings + wl * kRing);
+    lds_int *progL = (lds_int *)&H.prog[wl];
+    lds_int *consL = (lds_int *)&H.cons[wl];
+    const uint64_t *bin = a.bnd + sf.bnd_in;
+    uint64_t *bout = a.bnd + sl.bnd_out;
+    int copied = 0, drained = 0;
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
+    {
+        bool moved = false;
+        if (copied < nIn)
+        {
+            const int room = uniform(lds_ld(cons0)) + kRing - copied;  // free ring slots
+            const int want = min(min(kWave, nIn - copied), room);
+            if (want >= min(16, nIn - copied))
+            {
+                uint64_t probe = 0;
+                if (lane == 0) probe = load_granule(bin + copied + min(want, 16) - 1);
+                if ((uint32_t)uniform((int)(uint32_t)(probe >> 32)) == a.epoch)
+                {
+                    const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
+                    const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
+                    const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
+                    if (lane < cnt) lds_st(r0 + ring_slot(copied + lane + 1), (int)(uint32_t)v);
+                    copied += cnt;
+                    if (lane == 0) lds_st(prog0, copied);
+                    moved = cnt > 0;
+                }
+            }
+        }
+        if (drained < nOut)
+        {
+            const int avail = uniform(lds_ld(progL));
+            const int upto = min(avail, drained + kWave);
+            if (upto - drained >= 16 || (avail >= nOut && upto > drained))
+            {
+                const int c = drained + lane;
+                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)lds_ld(rl + ring_slot(c + 1)));
+                drained = upto;
+                if (lane == 0) lds_st(consL, drained);
+                moved = true;
+            }
+        }
+        if (moved)
+        {
+            t0 = __builtin_amdgcn_s_memrealtime();
+            continue;
+        }
+        for (int z = 0; z < a.io_sleep; ++z) __builtin_amdgcn_s_sleep(1);
+        if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
+        {
+            // release both sides so the group drains (the launch reports the abort)
+            if (lane == 0)
+            {
+                lds_st(prog0, nIn);
+                lds_st(consL, nOut + kRing);
+            }
+            return;
+        }
+    }
+}
+
+// One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
+// dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
+// predecessor has always been handed out before it: progress is guaranteed whatever the residency.
+template <int R, bool LOCAL, int SK, bool CHAIN>
+__global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs a)
+{
+    extern __shared__ int lds_dyn[];
+    GroupHdr &H = *reinterpret_cast<GroupHdr *>(lds_dyn);
+    lds_int *rings = (lds_int *)(lds_dyn + sizeof(GroupHdr) / 4);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = uniform((int)(threadIdx.x / kWave));
+    // compute waves; with CHAIN wave W is the I/O wave (plans without strip chains have none, and no
+    // rings in LDS either: more workgroups fit a CU)
+    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0);
+    if constexpr (SK == kTable)
+        for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
+    while (true)
+    {
+        __syncthreads();  // every wave is done with the previous group's rings
+        if (threadIdx.x == 0)
+        {
+            const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+            H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
+        }
+        if (threadIdx.x <= kMaxWaves)
+        {
+            H.prog[threadIdx.x] = 0;
+            H.cons[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        const int grp = uniform(H.group);
+        if (grp >= a.num_groups) break;
+        if (CHAIN && w == W)
+        {
+            io_wave(a, H, rings, grp, W, lane);
+        }
+        else
+        {
+            const int idx = grp * W + w;
+            if (idx < a.num_strips)
+            {
+                // the strip kind is compile-time inside process_strip (branch-free body boundaries)
+                // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
+                // variant is instantiated, which keeps the register count of the batch kernel down)
+                const int f = uniform(a.strips[idx].flags) & (kHasPrev | kHasNext);
+                if constexpr (CHAIN)
+                {
+                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, H, rings, idx, w, lane);
+                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, H, rings, idx, w, lane);
+                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, H, rings, idx, w, lane);
+                    else process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                }
+                else
+                {
+                    (void)f;
+                    process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                }
+            }
+        }
+    }
+}
+
+// Fill launches, one translation unit per strip height R (fill_r<R>.hip instantiates
+// launch_fill_r<R>; the main unit only declares them), so the 48 fill kernels compile in parallel.
+template <int R, bool LOCAL, int SK>
+void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t st)
+{
+    if (chain)
+    {
+        const size_t lds = std::max(group_lds_bytes(W), (size_t)a.chain_lds);
+        if (lds > 65536)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1)), lds, st, a);
+    }
+    else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
+}
+
+// R = 1 uses text profiles (kArr8 when the scores fit int8, kArr otherwise); taller strips use the
+// packed profile when the scores fit (kProf) and the LDS table otherwise (kTable).
+template <int R>
+void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st)
+{
+    if constexpr (R == 1)
+    {
+        if (sk == kArr8)
+        {
+            if (local) launch_fill_t<1, true, kArr8>(a, grid, W, chain, st);
+            else launch_fill_t<1, false, kArr8>(a, grid, W, chain, st);
+        }
+        else
+        {
+            if (local) launch_fill_t<1, true, kArr>(a, grid, W, chain, st);
+            else launch_fill_t<1, false, kArr>(a, grid, W, chain, st);
+        }
+    }
+    else if (sk == kPair)
+    {
+        if constexpr (R >= 16)
+            hipLaunchKernelGGL(fill_pair_kernel<R>, dim3(grid), dim3(kWave * W), 0, st, a);
+    }
+    else if (local)
+    {
+        if (sk == kProf) launch_fill_t<R, true, kProf>(a, grid, W, chain, st);
+        else launch_fill_t<R, true, kTable>(a, grid, W, chain, st);
+    }
+    else
+    {
+        if (sk == kProf) launch_fill_t<R, false, kProf>(a, grid, W, chain, st);
+        else launch_fill_t<R, false, kTable>(a, grid, W, chain, st);
+    }
+}
+
+template void launch_fill_r<SA_FILL_R>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+
+}  // namespace sa

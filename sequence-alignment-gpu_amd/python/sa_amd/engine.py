@@ -20,7 +20,7 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 # Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
-           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions")
+           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace")
 
 
 class SaParams(ctypes.Structure):
@@ -73,6 +73,7 @@ def _load():
     L.sa_device_count.argtypes = [ctypes.POINTER(I)]
     L.sa_last_error.restype = ctypes.c_char_p
     L.sa_selftest.argtypes = [I]
+    L.sa_release_workspace.argtypes = [I]
     for name in EXPORTS:
         getattr(L, name)
     return L
