@@ -111,6 +111,17 @@ int sa_plan_fetch_results(sa_plan *plan, sa_result *out, void *stream);
 int sa_plan_fetch_alignment(sa_plan *plan, int64_t index, char *aligned_text, char *aligned_pattern,
                             uint64_t cap, void *stream);
 
+/* Bytes of each of the plan's two aligned-string arenas (text and pattern side). */
+uint64_t sa_plan_output_bytes(const sa_plan *plan);
+
+/* Synchronise `stream` and copy every pair's result and both aligned-string arenas to host in one
+ * pass (what a batch caller needs: one copy each instead of one per pair). text_buf / pattern_buf
+ * hold buf_bytes >= sa_plan_output_bytes(plan) bytes; pair i's aligned text / pattern are the
+ * results[i].num_alignment_bytes letters at text_buf + offsets[i] / pattern_buf + offsets[i]
+ * (offsets: num_pairs entries). Returns SA_ERR_TIMEOUT if the fill aborted. */
+int sa_plan_fetch_all(sa_plan *plan, sa_result *results, char *text_buf, char *pattern_buf, uint64_t buf_bytes,
+                      uint64_t *offsets, void *stream);
+
 /* Introspection for benches and tests. */
 int sa_plan_info(const sa_plan *plan, int64_t *num_strips, int32_t *rows_per_lane,
                  uint64_t *device_bytes, uint64_t *mask_bytes);

@@ -868,6 +868,28 @@ int sa_plan_fetch_alignment(sa_plan *pl, int64_t index, char *at, char *ap, uint
     return SA_OK;
 }
 
+uint64_t sa_plan_output_bytes(const sa_plan *pl) { return pl ? pl->out_bytes : 0; }
+
+int sa_plan_fetch_all(sa_plan *pl, sa_result *out, char *tb, char *pb, uint64_t buf_bytes, uint64_t *offsets,
+                      void *stream)
+{
+    if (!pl || (!pl->pairs.empty() && (!out || !offsets))) return fail(SA_ERR_INVALID, "sa_plan_fetch_all: null argument");
+    if ((tb || pb) && buf_bytes < pl->out_bytes) return fail(SA_ERR_INVALID, "sa_plan_fetch_all: buffers below sa_plan_output_bytes");
+    hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
+    DeviceGuard dg(pl->device);
+    if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
+    Control ctrl;
+    HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
+    if (!pl->pairs.empty())
+        HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
+    if (tb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(tb, pl->d_out_text, pl->out_bytes, hipMemcpyDeviceToHost, st));
+    if (pb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(pb, pl->d_out_pattern, pl->out_bytes, hipMemcpyDeviceToHost, st));
+    for (size_t i = 0; i < pl->pairs.size(); ++i) offsets[i] = pl->pairs[i].out_off;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
+    return SA_OK;
+}
+
 int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *stream)
 {
     if (!pl || !M || index < 0 || index >= (int64_t)pl->pairs.size()) return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: bad argument");

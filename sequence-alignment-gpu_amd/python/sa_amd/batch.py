@@ -46,6 +46,9 @@ class DeviceBatch:
     def results(self) -> list[dict]:
         return self.plan.results(self.stream())
 
+    def all_alignments(self) -> list[dict]:
+        return self.plan.all_alignments(self.stream())
+
     def alignment(self, i: int) -> tuple[str, str]:
         return self.plan.alignment(i, self.stream())
 

@@ -20,7 +20,8 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 # Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
-           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace")
+           "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace",
+           "sa_plan_output_bytes", "sa_plan_fetch_all")
 
 
 class SaParams(ctypes.Structure):
@@ -74,6 +75,9 @@ def _load():
     L.sa_last_error.restype = ctypes.c_char_p
     L.sa_selftest.argtypes = [I]
     L.sa_release_workspace.argtypes = [I]
+    L.sa_plan_output_bytes.argtypes = [P]
+    L.sa_plan_output_bytes.restype = U64
+    L.sa_plan_fetch_all.argtypes = [P, ctypes.POINTER(SaResult), P, P, U64, P, P]
     for name in EXPORTS:
         getattr(L, name)
     return L
@@ -173,3 +177,19 @@ class Plan:
         _check(lib.sa_plan_fetch_alignment(self.handle, index, at, ap, cap, stream))
         r = self.results(stream)[index]
         return at.raw[: r["num_bytes"]].decode(), ap.raw[: r["num_bytes"]].decode()
+
+    def all_alignments(self, stream: int | None = None) -> list[dict]:
+        """Every pair's result with its aligned strings, fetched in one pass (sa_plan_fetch_all)."""
+        nb = int(lib.sa_plan_output_bytes(self.handle))
+        tb = np.empty(max(1, nb), np.uint8)
+        pb = np.empty(max(1, nb), np.uint8)
+        out = (SaResult * max(1, self.num_pairs))()
+        offs = np.zeros(max(1, self.num_pairs), np.uint64)
+        _check(lib.sa_plan_fetch_all(self.handle, out, tb.ctypes.data, pb.ctypes.data, max(1, nb),
+                                     offs.ctypes.data, stream))
+        res = []
+        for r, o in zip(out[: self.num_pairs], offs.tolist()):
+            L = r.num_alignment_bytes
+            res.append({"score": r.score, "num_bytes": L, "start_text": r.start_text, "start_pattern": r.start_pattern,
+                        "aligned_text": tb[o:o + L].tobytes().decode(), "aligned_pattern": pb[o:o + L].tobytes().decode()})
+        return res

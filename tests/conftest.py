@@ -72,3 +72,11 @@ def same_result(got: dict, exp: dict) -> bool:
 @pytest.fixture(scope="session")
 def golden():
     return {n: load(n) for n in ("known_answers.json", "data_pairs.json", "random_pairs.json", "large.json")}
+
+
+@pytest.fixture(scope="session")
+def eng():
+    """The HIP engine (ctypes over libsa_hip.so) after its wave-primitive self-test on device 0."""
+    from sa_amd import engine
+    engine.selftest(0)
+    return engine

@@ -16,12 +16,6 @@ from sa_amd import synthetic
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def eng():
-    from sa_amd import engine
-    engine.selftest(0)
-    return engine
-
 
 def _inputs(case):
     A = case["A"]
