@@ -129,6 +129,11 @@ uint64_t alignSequenceGPU(const Request &, Response *);
 /// -DBENCHMARK contract of the reference: DP fill only, returns its device time in microseconds.
 uint64_t alignSequenceGPUFillMicros(const Request &, Response *);
 
+/// Extension (the reference has no multi-GPU path): numRequests independent requests in one call,
+/// sharded over devices 0..numGpus-1 (sa_align_batch: one plan per device, RCCL result gather).
+/// Fills responses[i] as alignSequenceGPU would. Returns 0, or 1 with the message on stdout.
+uint64_t alignSequenceGPUBatch(const Request *requests, Response *responses, uint64_t numRequests, int numGpus);
+
 /// Host tracebacks over a full (m+1)x(n+1) byte DIRECTION matrix (used by the CPU device).
 void traceBackNW(const char *, const uint64_t, const uint64_t, const Request &, Response *);
 void traceBackSW(const char *, const uint64_t, const uint64_t, const uint64_t, const Request &, Response *);

@@ -87,6 +87,30 @@ int sa_align_pair(const sa_params *params, const char *text, uint64_t text_len,
  * are also released at process exit. */
 int sa_release_workspace(int device);
 
+/* ---- many pairs from host memory, sharded over GPUs ------------------------------------ */
+
+/* One pair in host memory (alphabet indices), as a Request holds it (SequenceAlignment.hpp:71-99). */
+typedef struct sa_host_pair {
+    const char *text;
+    uint64_t text_len;
+    const char *pattern;
+    uint64_t pattern_len;
+} sa_host_pair;
+
+/* Align num_pairs independent pairs with one scoring scheme over devices 0..num_gpus-1 of this
+ * process (one host thread and one plan per device; results gathered to device 0 with RCCL).
+ * Synchronous. results: num_pairs entries. aligned_text / aligned_pattern: NULL (scores only) or
+ * num_pairs host buffers, buffer i of at least text_len + pattern_len bytes, receiving pair i's
+ * num_alignment_bytes letters in forward order. The pair -> device deal is sa_batch_deal's. If
+ * num_gpus exceeds the device count, devices are shared round-robin (no RCCL then). */
+int sa_align_batch(const sa_params *params, const sa_host_pair *pairs, int64_t num_pairs, int num_gpus,
+                   sa_result *results, char *const *aligned_text, char *const *aligned_pattern);
+
+/* The deal sa_align_batch uses (host only, no device calls): shard_of[i] in 0..num_shards-1 for
+ * work cells[i] = text_len * pattern_len. Equal work: round-robin (i mod num_shards); otherwise
+ * longest-processing-time (largest first to the least-loaded shard, ties to the lower shard). */
+int sa_batch_deal(const uint64_t *cells, int64_t num_pairs, int num_shards, int32_t *shard_of);
+
 /* ---- plans: many pairs, device-resident inputs, explicit stream ------------------------- */
 
 /* Build a plan (strip layout, workspace) for num_pairs pairs on `device`. Allocates all device

@@ -4,7 +4,8 @@
 //   throughput global|local   DP fill only, best of N (benchmarks.cu:102-187: the -DBENCHMARK
 //                             contract, alignSequenceGPUFillMicros here), optional CPU fill
 //   latency    global|local   fill + traceback + result strings, end to end (:191-266)
-//   batch      N [global|local]  N 8192x8192 requests in sequence, end to end (:269-325)
+//   batch      N [global|local]  N 8192x8192 requests in sequence, end to end (:269-325); with
+//                             --multi G all N in one alignSequenceGPUBatch call over G devices
 //   maxlength  global|local   120000^2 and 500000^2, GPU fill only, no repeats (:328-355)
 //
 // Inputs are the reference's dummy requests (:21-41): protein, gap 5, BLOSUM50 from
@@ -34,6 +35,7 @@ namespace
 struct Options {
     bool cpu = false, gpu = true, json = false;
     int repeats = 5;
+    int multi = 0;  // batch: > 0 = one alignSequenceGPUBatch call over this many GPUs
     Sizes sizes;
 };
 
@@ -205,10 +207,16 @@ void batch(const Options &o, programArgs type, uint64_t nBatches)
         {
             SequenceAlignment::alignSequenceGPU(reqs[0], &gpuResp[0]);  // warmup
             const uint64_t t0 = now_us();
-            for (uint64_t i = 0; i < nBatches; ++i) SequenceAlignment::alignSequenceGPU(reqs[i], &gpuResp[i]);
+            if (o.multi > 0)
+            {
+                if (SequenceAlignment::alignSequenceGPUBatch(reqs.data(), gpuResp.data(), nBatches, o.multi))
+                    std::exit(1);
+            }
+            else
+                for (uint64_t i = 0; i < nBatches; ++i) SequenceAlignment::alignSequenceGPU(reqs[i], &gpuResp[i]);
             gpuTime = now_us() - t0;
             std::cout << "GPU = " << gpuTime / 1000 << " ms\n";
-            if (o.json) jsonLine("batch", type, rows, cols, "gpu", gpuTime, false);
+            if (o.json) jsonLine(o.multi > 0 ? "batch_multi" : "batch", type, rows, cols, "gpu", gpuTime, false);
         }
         if (o.cpu && o.gpu) std::cout << "GPU Speedup = " << (double)cpuTime / (double)gpuTime << "\n";
         for (auto &r : reqs) freeRequest(r);
@@ -255,7 +263,7 @@ int usage()
 {
     std::cerr << "usage: sa_benchmarks throughput|latency|maxlength global|local [opts]\n"
                  "       sa_benchmarks batch N [global|local] [opts]\n"
-                 "opts: --cpu --gpu --no-gpu --repeats N --sizes RxC,RxC --json\n";
+                 "opts: --cpu --gpu --no-gpu --repeats N --sizes RxC,RxC --json --multi G (batch: one call over G GPUs)\n";
     return 2;
 }
 }  // namespace
@@ -285,6 +293,7 @@ int main(int argc, const char *argv[])
         else if (a == "--json") o.json = true;
         else if (a == "--repeats" && i + 1 < argc) o.repeats = std::max(1, std::atoi(argv[++i]));
         else if (a == "--sizes" && i + 1 < argc) o.sizes = parseSizes(argv[++i]);
+        else if (a == "--multi" && i + 1 < argc) o.multi = std::max(1, std::atoi(argv[++i]));
         else return usage();
     }
     std::cout << "Benchmark on GPU: AMD Instinct MI355X (gfx950) via libsa_hip\n";

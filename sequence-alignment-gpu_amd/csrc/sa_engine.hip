@@ -118,6 +118,14 @@ int fail(int code, const std::string &msg)
     return code;
 }
 
+}  // namespace
+
+namespace sa {
+int set_error(int code, const std::string &msg) { return fail(code, msg); }
+}  // namespace sa
+
+namespace {
+
 #define HIP_TRY(expr)                                                                        \
     do {                                                                                     \
         hipError_t e_ = (expr);                                                              \

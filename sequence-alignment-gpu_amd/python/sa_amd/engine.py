@@ -21,7 +21,7 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
            "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace",
-           "sa_plan_output_bytes", "sa_plan_fetch_all")
+           "sa_plan_output_bytes", "sa_plan_fetch_all", "sa_align_batch", "sa_batch_deal")
 
 
 class SaParams(ctypes.Structure):
@@ -78,6 +78,8 @@ def _load():
     L.sa_plan_output_bytes.argtypes = [P]
     L.sa_plan_output_bytes.restype = U64
     L.sa_plan_fetch_all.argtypes = [P, ctypes.POINTER(SaResult), P, P, U64, P, P]
+    L.sa_align_batch.argtypes = [ctypes.POINTER(SaParams), P, ctypes.c_int64, I, ctypes.POINTER(SaResult), P, P]
+    L.sa_batch_deal.argtypes = [P, ctypes.c_int64, I, P]
     for name in EXPORTS:
         getattr(L, name)
     return L
@@ -123,6 +125,45 @@ def align_pair(mode: int, text: np.ndarray, pattern: np.ndarray, S: np.ndarray, 
     L = res.num_alignment_bytes
     return {"score": res.score, "num_bytes": L, "start_text": res.start_text, "start_pattern": res.start_pattern,
             "aligned_text": at.raw[:L].decode(), "aligned_pattern": ap.raw[:L].decode(), "fill_us": fill_us.value}
+
+
+class SaHostPair(ctypes.Structure):
+    _fields_ = [("text", ctypes.c_void_p), ("text_len", ctypes.c_uint64), ("pattern", ctypes.c_void_p),
+                ("pattern_len", ctypes.c_uint64)]
+
+
+def batch_deal(cells: list[int], num_shards: int) -> list[int]:
+    """sa_batch_deal: the pair -> shard assignment sa_align_batch uses (host only)."""
+    c = np.ascontiguousarray(cells, dtype=np.uint64)
+    out = np.zeros(max(1, len(c)), np.int32)
+    _check(lib.sa_batch_deal(c.ctypes.data, len(c), num_shards, out.ctypes.data))
+    return out[: len(c)].tolist()
+
+
+def align_batch(mode: int, texts: list[np.ndarray], patterns: list[np.ndarray], S: np.ndarray, gap: int,
+                num_gpus: int = 1, alphabet: bytes | None = None, strings: bool = True) -> list[dict]:
+    """sa_align_batch: independent pairs from host memory over devices 0..num_gpus-1 (synchronous)."""
+    p, S_keep, alpha_keep = _params(mode, S, gap, alphabet, 0)
+    ts = [np.ascontiguousarray(t, dtype=np.int8) for t in texts]
+    ps = [np.ascontiguousarray(x, dtype=np.int8) for x in patterns]
+    n = len(ts)
+    hp = (SaHostPair * max(1, n))(*[SaHostPair(t.ctypes.data, len(t), x.ctypes.data, len(x)) for t, x in zip(ts, ps)])
+    bufs_t = [ctypes.create_string_buffer(max(1, len(t) + len(x))) for t, x in zip(ts, ps)] if strings else []
+    bufs_p = [ctypes.create_string_buffer(max(1, len(t) + len(x))) for t, x in zip(ts, ps)] if strings else []
+    at = (ctypes.c_void_p * max(1, n))(*[ctypes.addressof(b) for b in bufs_t]) if strings else None
+    ap = (ctypes.c_void_p * max(1, n))(*[ctypes.addressof(b) for b in bufs_p]) if strings else None
+    res = (SaResult * max(1, n))()
+    _check(lib.sa_align_batch(ctypes.byref(p), hp, n, num_gpus, res, at, ap))
+    out = []
+    for i, r in enumerate(res[:n]):
+        d = {"score": r.score, "num_bytes": r.num_alignment_bytes, "start_text": r.start_text,
+             "start_pattern": r.start_pattern}
+        if strings:
+            L = r.num_alignment_bytes
+            d["aligned_text"] = bufs_t[i].raw[:L].decode()
+            d["aligned_pattern"] = bufs_p[i].raw[:L].decode()
+        out.append(d)
+    return out
 
 
 class Plan:
