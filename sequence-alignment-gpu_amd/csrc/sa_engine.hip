@@ -32,10 +32,26 @@ namespace sa {
 //   kProf / kTable  one dword per letter, 8*c (packed-profile bit offset) or c (LDS table index);
 //   kArr            A dword arrays of code_len: array a holds table[a][t[x]] at kPad + x;
 //   kArr8           4A byte arrays of code_len bytes: copy (a, r) holds table[a][t[x]] at kPad + x + r.
-__global__ void encode_text_kernel(const int8_t *text, const PairDesc *pairs, int32_t *codes, int A, int SK,
-                                   const int32_t *table)
+__global__ void encode_text_kernel(const int8_t *text, const int8_t *pattern, const PairDesc *pairs, int32_t *codes,
+                                   int A, int SK, const int32_t *table, Control *ctrl)
 {
     const PairDesc pd = pairs[blockIdx.y];
+    // the arenas must hold alphabet indices 0..A-1 (Request::textBytes / patternBytes are indices,
+    // utilities.cpp:52); the kernels clamp, so a bad byte is reported instead of aligned silently
+    bool bad = false;
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.pattern_len;
+         x += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const int c = pattern[pd.pattern_off + x];
+        bad = bad || c < 0 || c >= A;
+    }
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
+         x += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const int c = text[pd.text_off + x];
+        bad = bad || c < 0 || c >= A;
+    }
+    if (bad) __hip_atomic_store(&ctrl->bad_input, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (SK == kPair)
     {
         // selectors of pairs (2q, 2q+1) in pair 2q's block, padding included (0x0c0c0c0c = zeros)
@@ -702,14 +718,15 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
     if (np > 0)
     {
         uint64_t nmax = 1;
-        for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, d.text_len);
+        for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, std::max(d.text_len, d.pattern_len));
         const int gx = (int)std::min<uint64_t>((nmax + 255) / 256, 64);
         for (int y0 = 0; y0 < np; y0 += 65534)
         {
             // pairs beyond 65535 are handled by re-basing the pair pointer
             const int cnt = std::min(65534, np - y0);  // even: kPair pairs (2q, 2q+1) stay in one launch
             hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
-                               pl->d_pairs + y0, pl->d_codes, pl->A, pl->sk, pl->d_table);
+                               (const int8_t *)d_pattern, pl->d_pairs + y0, pl->d_codes, pl->A, pl->sk, pl->d_table,
+                               pl->d_ctrl);
         }
         HIP_TRY(hipGetLastError());
         if (int rc = debug_sync(st, "encode_text_kernel")) return rc;
@@ -852,6 +869,7 @@ int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
     if (!pl->pairs.empty())
         HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     return SA_OK;
 }
@@ -894,6 +912,7 @@ int sa_plan_fetch_all(sa_plan *pl, sa_result *out, char *tb, char *pb, uint64_t 
     if (pb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(pb, pl->d_out_pattern, pl->out_bytes, hipMemcpyDeviceToHost, st));
     for (size_t i = 0; i < pl->pairs.size(); ++i) offsets[i] = pl->pairs[i].out_off;
     HIP_TRY(hipStreamSynchronize(st));
+    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     return SA_OK;
 }
@@ -996,6 +1015,7 @@ int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *
     HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     // also in fill-only mode: a fill whose hand-off timed out produced garbage, not a fill time
+    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     if (fill_us)
     {

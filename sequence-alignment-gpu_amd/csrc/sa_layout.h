@@ -58,7 +58,8 @@ struct PairDesc {
 struct Control {
     uint32_t queue_head;   // dynamic strip queue
     uint32_t abort_flag;   // set when a hand-off times out
-    uint32_t pad[2];
+    uint32_t bad_input;    // set by encode_text_kernel: a text or pattern byte outside 0..A-1
+    uint32_t pad;
 };
 
 }  // namespace sa
