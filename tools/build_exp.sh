@@ -7,10 +7,10 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 src=$root/sequence-alignment-gpu_amd/csrc
 out=/tmp/sa_build_exp/$tag
 mkdir -p "$out"
-flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include -I$src $*"
+flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include -I$src -DSA_EXPERIMENT=1 $*"
 # EXP_ONLY="fill_r1 ..." recompiles only those units and takes the others from the product build
 pids=()
-for f in sa_engine fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
+for f in sa_engine sa_walk sa_batch fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
   if [ -n "$EXP_ONLY" ] && [[ " $EXP_ONLY " != *" $f "* ]]; then
     cp $root/sequence-alignment-gpu_amd/build/$f.o $out/$f.o
   else
@@ -18,5 +18,6 @@ for f in sa_engine fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
   fi
 done
 for p in "${pids[@]}"; do wait $p; done
-/opt/rocm/bin/hipcc $flags -shared $out/*.o -o $root/build_exp/libsa_$tag.so
+mkdir -p $root/build_exp
+/opt/rocm/bin/hipcc $flags -shared $out/*.o -L/opt/rocm/lib -lrccl -o $root/build_exp/libsa_$tag.so
 echo built build_exp/libsa_$tag.so

@@ -40,6 +40,9 @@ def main():
     args = ap.parse_args()
     if args.waves:
         os.environ["SA_WAVES_PER_GROUP"] = str(args.waves)
+    # the engine reads its knobs once per process: every fill of this process dumps its timeline
+    path = os.path.join(tempfile.mkdtemp(), "tl.bin")
+    os.environ["SA_TIMELINE"] = path
     from sa_amd import synthetic
     from sa_amd.batch import DeviceBatch
     S = synthetic.blast_matrix()
@@ -48,10 +51,7 @@ def main():
     b = DeviceBatch(args.mode, S, 5, [t] * args.pairs, [p] * args.pairs, rows_per_lane=args.R)
     b.fill()
     b.fill()
-    path = os.path.join(tempfile.mkdtemp(), "tl.bin")
-    os.environ["SA_TIMELINE"] = path
-    b.fill()
-    del os.environ["SA_TIMELINE"]
+    b.fill()  # the file holds the last fill's timeline
     import torch
     torch.cuda.synchronize()
     tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 6)
