@@ -574,7 +574,9 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         const uint64_t n = d.text_len, m = d.pattern_len;
         const int ns = (n == 0 || m == 0) ? 0 : (int)((m + RB - 1) / RB);
         d.num_strips = ns;
-        const int nsteps = (int)(((n + kWave - 1) + 2 * U - 1) / (2 * U) * (2 * U));  // two bodies per loop trip
+        // n + 63 steps reach column n in lane 63; one more step moves its bottom-row value into the
+        // publishing register (sa_fill.hip run_body); two bodies per loop trip
+        const int nsteps = (int)(((n + kWave) + 2 * U - 1) / (2 * U) * (2 * U));
         for (int b = 0; b < ns; ++b)
         {
             StripDesc s;

@@ -62,6 +62,15 @@ typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, nev
 // LDS executes one wave's ds operations in order, which is the only ordering the rings rely on.
 __device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// LDS read and wait in one statement (slow paths: the register cannot be touched before the data
+// is there, and the compiler's waitcnt pass sees no pending LDS load it would have to merge into the
+// fast path's state; a compiler-visible read here put an s_waitcnt lgkmcnt(0) at every body's top)
+__device__ __forceinline__ int ds_read_sync(const lds_int *p)
+{
+    int v;
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+    return v;
+}
 constexpr int kRing = 2048;        // ring entries (columns), power of two
 constexpr int kRingMask = kRing - 1;
 #ifndef SA_CODE_AHEAD
@@ -79,10 +88,10 @@ constexpr int kRingMask = kRing - 1;
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
-    int prog[kMaxWaves + 1];       // prog[w]: columns published into ring[w]
     int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
     int group;                     // group index taken from the queue
-    int pad[1];
+    int pad[2];
+    int dummy[kMaxWaves][kWave];   // publish target of the lanes that carry no bottom-row value
 };
 __host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + (size_t)(W + 1) * kRing * 4; }
 
@@ -97,28 +106,17 @@ __device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int
     return !(aborted || late);
 }
 
-// Waits until the producer wave has published columns 1..need into the ring (LDS progress word),
-// or until the fill is aborted (timeout): the strip then runs on with whatever the ring holds and
-// the launch reports the abort, so the hot loop carries no error-path control flow.
-__device__ __forceinline__ void wait_ring(const FillArgs &a, lds_int *prog, int need, int &avail, int lane)
-{
-    avail = uniform(lds_ld(prog));
-    if (avail >= need) return;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t spin = 1;; ++spin)
-    {
-        __builtin_amdgcn_s_sleep(1);
-        avail = uniform(lds_ld(prog));
-        if (avail >= need) return;
-        if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) return;
-    }
-}
-
-// Ring slot of column c (1-based) in every LDS ring. The +14 puts the first column of a producer
-// body's bottom-row values (c = s0 - 62, s0 a multiple of U) on a slot that is a multiple of U, so
-// lane 63 publishes a body with U/4 ds_write_b128 that never straddle the ring's end.
-__device__ __forceinline__ int ring_slot(int c) { return (c + 14) & kRingMask; }
-static_assert(kRing % 16 == 0, "ring must hold whole bodies");
+// Ring slot of column c (1-based) in every LDS ring, and the tag its entry carries in bit 31.
+// Entries are self-validating: a value (always in [0, 2^30)) is stored with bit 31 =
+// the complement of its lap's parity, lap = (c + 63) / kRing, so a reader needs no progress word: a
+// slot holds column c exactly when its tag is c's (the zeroed ring of a new group matches no lap-0
+// column; a slot still holding the previous lap's column has the other parity). The +63 makes a
+// producer body's columns (s0 - 63 .. s0 - 64 + U, s0 a multiple of U) one aligned run of slots
+// inside one lap, so its tag is uniform.
+__device__ __forceinline__ int ring_slot(int c) { return (c + 63) & kRingMask; }
+__device__ __forceinline__ int ring_tag(int c) { return (int)((((uint32_t)(c + 63) >> 11) & 1u) ^ 1u) << 31; }
+static_assert(kRing == 2048, "ring_tag assumes 2048-entry rings");
+constexpr int kConsEvery = 256;  // a consumer publishes its consumption word every this many columns
 
 
 // a + sign_extend(byte B of w), one VALU op
@@ -162,20 +160,22 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
 // wave_shr:1 whose `old` operand is this step's feed register Q (lane 0 keeps Q's lane 0 = the
 // strip above's bottom value for this column); Q is dead afterwards, so the DPP writes in place. The
-// next step's feed register is Q shifted down one lane (wave_shl:1, bound_ctrl), computed first.
-// The strip's bottom row (F[R-1] of lane 63 after each step) is not moved at all: every step's F[R-1]
-// stays in its own register Fs[q] until the body ends, when lane 63 publishes all U of them.
-template <int R, bool LOCAL, int SK, int KIND>
+// next step's feed register is Q shifted down one lane (wave_shl:1), computed first. With a strip
+// below (HN) that shift's `old` is F[R-1], so lane 63 takes in the previous step's bottom-row value:
+// after U steps lanes 64-U..63 of Q hold the bottom row of steps s0-1 .. s0+U-2, and one full-wave
+// ds_write publishes them (the other lanes write a dummy slot). Steps [QB, QE) of the body.
+template <int R, bool LOCAL, int SK, int KIND, bool HN, int QB, int QE>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Codes<R, SK>::NT],
-                                         int (&F)[R], int (&best)[R], int &upPrev, int Q,
-                                         int (&Fs)[Cfg<R>::U], uint32_t (&acc)[3][Cfg<R>::NW])
+                                         int (&F)[R], int (&best)[R], int &upPrev, int &Q,
+                                         uint32_t (&acc)[3][Cfg<R>::NW])
 {
-    constexpr int U = Cfg<R>::U;
-    sfor<U>([&](auto Qc) {
-        constexpr int q = decltype(Qc)::value;
+    sfor<QE - QB>([&](auto Qc) {
+        constexpr int q = QB + decltype(Qc)::value;
         const int s = s0 + q;
-        const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
+        int Qn;
+        if constexpr (HN) Qn = dpp_shl1(F[R - 1], Q);                         // lane 63 <- bottom row
+        else Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);         // wave_shl:1
         int up = dpp_shr1(Q, F[R - 1]);
         Q = Qn;
         int diag = upPrev;
@@ -227,7 +227,6 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
             up = Fn;
             F[rho] = Fn;
         });
-        Fs[q] = F[R - 1];
     });
 }
 
@@ -314,10 +313,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         coff = (uint32_t)((kPad - lane) * 4);
     lds_int *rin = (lds_int *)(rings + w * kRing);
     lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
-    lds_int *progIn = (lds_int *)&H.prog[w];
     lds_int *consIn = (lds_int *)&H.cons[w];
-    lds_int *progOut = (lds_int *)&H.prog[w + 1];
     lds_int *consOut = (lds_int *)&H.cons[w + 1];
+    // publishing lanes (64-U..63) and their column offset; the others write their own dummy slot
+    const bool pubLane = lane >= kWave - U;
+    const int pubRel = lane - (kWave - U);
+    lds_int *pubDummy = (lds_int *)&H.dummy[w][lane];
     // the strip's direction chunks (uniform base) and this lane's byte offset in a chunk
     uint32_t *mbase = a.masks + sd.mask_off * 4;
     const uint32_t moff = (uint32_t)(lane * Cfg<R>::LW * 4);
@@ -342,7 +343,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         best[rho] = 0;
     });
     int upPrev = 0, Q = 0;
-    int Fs[U];
     // text codes, double-buffered across the two bodies of a pair (no register copies)
     // text codes: SA_CODE_AHEAD = 1 double-buffers across the two bodies of a pair; 2 keeps four
     // buffers and loads every body's codes two bodies ahead (bodies run in quads)
@@ -360,33 +360,24 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             dst[q + 3] = v.w;
         });
     };
-    const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
-    load_codes(0, TA);
-    if constexpr (kAhead == 2) load_codes(U, TB);
-    int avail = 0;       // columns known to be in rin
     int consKnown = 0;   // columns the consumer of rout is known to have read
-    // The progress word and the feed values for body k+2 are read speculatively at the end of body
-    // k and used at the end of body k+1 without an LDS round trip (LDS is in order per wave: values
-    // read after a progress word that covers them are valid). At a body boundary the order is feed
-    // check -> next prefetch -> publish -> consumption word: the only LDS wait (the feed check, one
-    // body after its reads) never waits for a boundary's writes. Feeds and publications are not
-    // masked at the ends of the text: values of columns <= 0 or > n only ever reach cells outside
-    // [1, n].
-    int pfProg = 0, pfVal = 0;
+    // Feed values for the body starting at step base (columns base+1 .. base+U, lanes 0..U-1 of Q)
+    // are read kPfLead steps before that body starts, in the middle of the previous body: early
+    // enough to cover the LDS latency, late enough that the strip above has published them by then
+    // without the chain growing a body of lag per strip (a read one body ahead costs U steps of lag).
+    // The read is checked at the boundary by the entries' tags (ring_tag); a slot not yet written
+    // sends the wave to the slow path, which re-reads until every needed lane is there.
+    int pfVal = 0;
     auto prefetch = [&](int base) __attribute__((always_inline)) {
-        if constexpr (HP && SA_ABL != 1)
+        if constexpr (HP)
         {
-            pfProg = lds_ld(progIn);
-            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
+            int c = base + 1 + lane;
+            // the read may not move above the steps before this point (the compiler would hoist it)
+            asm volatile("" : "+v"(c) : "v"(F[R - 1]));
+            pfVal = lds_ld(rin + ring_slot(c));
         }
     };
-    // lanes 0..U-1 of Q take the bottom values of columns base+1 .. base+U of the strip above
     auto feed = [&](int base) __attribute__((always_inline)) {
-        if constexpr (SA_ABL != 0)
-        {
-            Q = pfVal;  // timing ablation (development only): never waits, results are garbage
-            return;
-        }
         if constexpr (!HP)
         {
             // row 0 boundary. The zero is opaque on purpose: with a known-zero `old` the compiler
@@ -395,30 +386,67 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             asm volatile("v_mov_b32 %0, 0" : "=v"(Q));
             return;
         }
-        const int need = min(n, base + U);
-        if (__builtin_expect(uniform(pfProg) < need, 0))
+        else
         {
-            wait_ring(a, progIn, need, avail, lane);
-            pfVal = lds_ld(rin + ring_slot(base + 1 + lane));
+            // lanes 0..cnt-1 carry columns base+1 .. base+cnt <= n; one aligned run: one tag
+            const int tag = ring_tag(base + 1);
+            const int cnt = min(max(n - base, 0), U);
+            const uint64_t need = (1ull << cnt) - 1;
+            int x = pfVal ^ tag;
+            if (__builtin_expect((ballot(x < 0) & need) != 0, 0))
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    __builtin_amdgcn_s_sleep(1);
+                    x = ds_read_sync(rin + ring_slot(base + 1 + lane)) ^ tag;
+                    if ((ballot(x < 0) & need) == 0) break;
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+                }
+            }
+            Q = x;  // lanes >= cnt: don't care
+            const int upto = base + U;
+            if (((upto & (kConsEvery - 1)) == 0) && lane == 0) lds_st(consIn, upto);
         }
-        Q = pfVal;  // lanes >= U: don't care
     };
-    auto consumed = [&](int upto) __attribute__((always_inline)) {
-        if constexpr (HP && SA_ABL != 1)
-            if (lane == 0) lds_st(consIn, upto);
+    // lanes 64-U..63 of Q hold the bottom row of columns s0-63 .. s0-64+U: one ds_write_b32 by every
+    // lane (the others to their dummy slot), tagged, after making sure the consumer has read the
+    // slots' previous lap
+    auto publish = [&](int s0) __attribute__((always_inline)) {
+        if constexpr (HN)
+        {
+            const int cLast = s0 - 64 + U;
+            if (__builtin_expect(cLast - kRing > consKnown, 0))
+            {
+                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    consKnown = uniform(lds_ld(consOut));
+                    if (cLast - kRing <= consKnown) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+                }
+            }
+            lds_int *dst = pubLane ? rout + ((s0 + pubRel) & kRingMask) : pubDummy;
+            lds_st(dst, Q | ring_tag(s0 - 63));
+        }
     };
+    const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    load_codes(0, TA);
+    if constexpr (kAhead == 2) load_codes(U, TB);
     prefetch(0);
     feed(0);
-    consumed(U);
-    prefetch(U);
     const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
+    constexpr int kPfLead = U >= 8 ? U / 4 : 1;  // steps between the feed read and its use
     auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
         constexpr int KIND = decltype(kind)::value;
         const int s1 = s0 + U;
         load_codes(s0 + kAhead * U, Tn);
-        run_body<R, LOCAL, SK, KIND>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, Fs, acc);
+        run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+        prefetch(s1);
+        run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
         if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
@@ -449,51 +477,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 });
             }
         }
-        // (after the last body this waits for the strip above's final progress word, n)
-        // The prefetched words must not be read before the body's steps: left alone, the compiler
-        // hoists the feed check (and its LDS wait) above the body, stalling right after the prefetch
-        // and asking for the strip above's values a body early.
-        if constexpr (HP) asm volatile("" : "+v"(pfProg), "+v"(pfVal) : "v"(Fs[U - 1]));
+        publish(s0);
         feed(s1);
-#if SA_PF_FIRST
-        prefetch(s1 + U);  // reads before this boundary's writes: waiting for them never waits for the writes
-#endif
-        if constexpr (HN && SA_ABL != 1)
-        {
-            // lane 63's Fs[q] is the bottom-row value of column c0 + q (lane 63 is on column s-62);
-            // ring slots of columns c0..c0+U-1 must have been read: c - kRing <= consumed
-            const int c0 = s0 - (kWave - 2);
-            const int top = min(n, max(0, s1 - 1 - (kWave - 2)));
-            if (__builtin_expect(c0 + U - 1 - kRing > consKnown, 0))
-            {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                for (uint32_t spin = 1;; ++spin)
-                {
-                    consKnown = uniform(lds_ld(consOut));
-                    if (c0 + U - 1 - kRing <= consKnown) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
-                }
-            }
-            if (lane == kWave - 1)
-            {
-                typedef int i32x4 __attribute__((ext_vector_type(4)));
-                typedef __attribute__((address_space(3))) i32x4 lds_i32x4;
-                lds_i32x4 *dst = (lds_i32x4 *)(rout + ring_slot(c0));
-                sfor<U / 4>([&](auto Xc) {
-                    constexpr int x = decltype(Xc)::value;
-                    dst[x] = i32x4{Fs[4 * x], Fs[4 * x + 1], Fs[4 * x + 2], Fs[4 * x + 3]};
-                });
-                // the values go before the progress word: a compiler-only fence (LDS executes one
-                // wave's operations in order)
-                asm volatile("" ::: "memory");
-                lds_st(progOut, top);
-            }
-        }
-        consumed(s1 + U);
-#if !SA_PF_FIRST
-        prefetch(s1 + U);
-#endif
     };
     using KSteady = std::integral_constant<int, kSteady>;
     using KStart = std::integral_constant<int, kStart>;
@@ -550,7 +535,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             body(KGeneric{}, Second{}, s0 + U, TB, TA);
         }
     }
-    if (HN && lane == kWave - 1) lds_st(progOut, n);  // never leave the consumer waiting (abort)
     if (a.timeline && lane == 0)
     {
         uint64_t *tl = a.timeline + kTimelineWords * (size_t)idx;
@@ -776,7 +760,8 @@ __global__ __launch_bounds__(kWave * kMaxWaves, 2) void fill_pair_kernel(FillArg
 // The I/O wave of a group: global granules of the previous group's last strip -> ring[0], and
 // ring[W'] (W' = compute waves with a strip) -> granules for the next group. Only lane 0 polls the
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
-// load the fabric the running strips use); the bytes move 64 columns per instruction.
+// load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
+// carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
 __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
@@ -788,20 +773,22 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
     if (nIn == 0 && nOut == 0) return;
     const int wl = last - first + 1;  // ring fed by the last strip
     lds_int *r0 = (lds_int *)rings;
-    lds_int *prog0 = (lds_int *)&H.prog[0];
     lds_int *cons0 = (lds_int *)&H.cons[0];
     lds_int *rl = (lds_int *)(rings + wl * kRing);
-    lds_int *progL = (lds_int *)&H.prog[wl];
     lds_int *consL = (lds_int *)&H.cons[wl];
     const uint64_t *bin = a.bnd + sf.bnd_in;
     uint64_t *bout = a.bnd + sl.bnd_out;
     int copied = 0, drained = 0;
+    // slots of columns -63..0 are never copied in: give them their lap-0 tag, or the zeroed entries
+    // would pass for lap-1 columns 1985..2048 (a compute-wave producer publishes from column -63)
+    if (nIn > 0) lds_st(r0 + ring_slot(lane - 63), ring_tag(lane - 63));
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
     {
         bool moved = false;
         if (copied < nIn)
         {
+            // ring[0]'s consumer publishes its consumption every kConsEvery columns
             const int room = uniform(lds_ld(cons0)) + kRing - copied;  // free ring slots
             const int want = min(min(kWave, nIn - copied), room);
             if (want >= min(16, nIn - copied))
@@ -813,21 +800,22 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
                     const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
                     const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
                     const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
-                    if (lane < cnt) lds_st(r0 + ring_slot(copied + lane + 1), (int)(uint32_t)v);
+                    const int c = copied + lane + 1;
+                    if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
                     copied += cnt;
-                    if (lane == 0) lds_st(prog0, copied);
                     moved = cnt > 0;
                 }
             }
         }
         if (drained < nOut)
         {
-            const int avail = uniform(lds_ld(progL));
-            const int upto = min(avail, drained + kWave);
-            if (upto - drained >= 16 || (avail >= nOut && upto > drained))
+            const int c = drained + lane + 1;
+            const int x = lds_ld(rl + ring_slot(c)) ^ ring_tag(c);
+            const uint64_t rdy = ballot(x >= 0 && c <= nOut);
+            const int upto = drained + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
+            if (upto - drained >= 16 || (upto >= nOut && upto > drained))
             {
-                const int c = drained + lane;
-                if (c < upto) store_granule(bout + c, ((uint64_t)a.epoch << 32) | (uint32_t)lds_ld(rl + ring_slot(c + 1)));
+                if (c <= upto) store_granule(bout + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
                 drained = upto;
                 if (lane == 0) lds_st(consL, drained);
                 moved = true;
@@ -841,12 +829,9 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
         for (int z = 0; z < a.io_sleep; ++z) __builtin_amdgcn_s_sleep(1);
         if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
         {
-            // release both sides so the group drains (the launch reports the abort)
-            if (lane == 0)
-            {
-                lds_st(prog0, nIn);
-                lds_st(consL, nOut + kRing);
-            }
+            // release the producer so the group drains (the launch reports the abort; ring[0]'s
+            // consumer gives up by itself)
+            if (lane == 0) lds_st(consL, nOut + kRing);
             return;
         }
     }
@@ -876,10 +861,13 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
             const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
         }
-        if (threadIdx.x <= kMaxWaves)
+        if (threadIdx.x <= kMaxWaves) H.cons[threadIdx.x] = 0;
+        if constexpr (CHAIN)
         {
-            H.prog[threadIdx.x] = 0;
-            H.cons[threadIdx.x] = 0;
+            // tags: a zeroed ring matches no column (ring_tag)
+            typedef int i32x4 __attribute__((ext_vector_type(4)));
+            for (int e = 4 * threadIdx.x; e < (W + 1) * kRing; e += 4 * blockDim.x)
+                *(__attribute__((address_space(3))) i32x4 *)(rings + e) = i32x4{0, 0, 0, 0};
         }
         __syncthreads();
         const int grp = uniform(H.group);

@@ -232,3 +232,27 @@ def test_very_long_reference_cases(eng):
         at, ap = got["aligned_text"], got["aligned_pattern"]
         assert _score_of(at, ap, S, case["gap"], A) == got["score"], case["name"]
         assert at.replace("-", "") == case["text"] and ap.replace("-", "") == case["pattern"], case["name"]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_chain_ring_laps_across_groups(eng, mode):
+    """Strip chains whose hand-off rings wrap one to three times (text > 2048 columns), in plans where
+    the W-strip groups start at every strip offset of a pair (the first strip of a group is fed by the
+    I/O wave, the others by their neighbour wave): every pair bit-exact, every cell of two pairs."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    shapes = [(2100, 300), (4200, 650), (6300, 450), (2049, 130), (3000, 200)]
+    texts = [synthetic.random_sequence(1300 + k, n, 4) for k, (n, _) in enumerate(shapes)]
+    pats = [synthetic.mutate(t, 1400 + k, 4, m) for k, (t, (_, m)) in enumerate(zip(texts, shapes))]
+    b = DeviceBatch(mode, S, 5, texts, pats, rows_per_lane=1)
+    b.fill()
+    b.traceback()
+    got = b.all_alignments()
+    for k in range(len(shapes)):
+        assert got[k] == oracle.align(mode, texts[k], pats[k], S, 5), (mode, shapes[k])
+    for k in (1, 4):
+        n, m = shapes[k]
+        exp = np.empty((m + 1) * (n + 1), np.uint8)
+        oracle.fill_only(mode, texts[k], pats[k], S, 5, exp)
+        assert int((b.directions(k) != exp).sum()) == 0, shapes[k]
+    b.close()
