@@ -766,7 +766,8 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * kTimelineWords * ns));
             tlBuf.reset(a.timeline);
         }
-        const int W = pl->W;
+        // (the pair-packed kernel always runs kPairWaves waves per workgroup)
+        const int W = pl->sk == kPair ? kPairWaves : pl->W;
         a.num_groups = (ns + W - 1) / W;
         // chains: two workgroups of W compute waves + an I/O wave per CU; lone strips: W compute
         // waves per workgroup and up to 16 waves per CU (the batch kernel stays under 128 VGPRs)

@@ -37,7 +37,9 @@ struct FillArgs {
 };
 
 constexpr int kTimelineWords = 6;  // SA_TIMELINE record per strip
-constexpr int kMaxWaves = 4;       // compute waves per workgroup (+1 I/O wave: 320 threads, <= 256 VGPRs)
+constexpr int kMaxWaves = 4;       // compute waves per chain workgroup (+1 I/O wave: 320 threads; one
+                                   // compute wave per SIMD: two per SIMD ran 2.2x slower per step)
+constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed batch kernel
 
 // Where a strip's substitution scores come from (SK). Every table already holds S + 2g (global) or
 // S + g (local), the offsets the recurrences below fold in:

@@ -62,13 +62,15 @@ typedef __attribute__((address_space(3))) int lds_int;  // ds_read/ds_write, nev
 // LDS executes one wave's ds operations in order, which is the only ordering the rings rely on.
 __device__ __forceinline__ int lds_ld(lds_int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void lds_st(lds_int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ uint32_t lds_off(const lds_int *p) { return (uint32_t)(uintptr_t)p; }
+__device__ __forceinline__ void ds_write_async(lds_int *p, int v) { asm volatile("ds_write_b32 %0, %1" ::"v"(lds_off(p)), "v"(v)); }
 // LDS read and wait in one statement (slow paths: the register cannot be touched before the data
 // is there, and the compiler's waitcnt pass sees no pending LDS load it would have to merge into the
 // fast path's state; a compiler-visible read here put an s_waitcnt lgkmcnt(0) at every body's top)
 __device__ __forceinline__ int ds_read_sync(const lds_int *p)
 {
     int v;
-    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"((uint32_t)(uintptr_t)p));
+    asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_off(p)));
     return v;
 }
 constexpr int kRing = 2048;        // ring entries (columns), power of two
@@ -82,6 +84,9 @@ constexpr int kRingMask = kRing - 1;
 #ifndef SA_ABL
 #define SA_ABL 0  // timing ablations of the hand-off (development builds only; results are wrong)
 #endif
+#ifndef SA_FILL_ASM
+#define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body, for A/B)
+#endif
 #ifndef SA_CODE_AHEAD_LOCAL
 #define SA_CODE_AHEAD_LOCAL 2
 #endif
@@ -90,17 +95,31 @@ struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
     int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
     int group;                     // group index taken from the queue
-    int pad[2];
-    int dummy[kMaxWaves][kWave];   // publish target of the lanes that carry no bottom-row value
+    int nwaves;                    // compute waves of the workgroup (W)
+    int pad[1];
 };
-__host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + (size_t)(W + 1) * kRing * 4; }
+// chain workgroup LDS: header, W + 1 rings, then one shared sink that the lanes carrying no
+// bottom-row value write into when their wave publishes (a ring's size plus a wave, so that a
+// lane's sink slot is its ring slot offset: the publish address is one add per body)
+constexpr int kSink = kRing + kWave;
+__host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + ((size_t)(W + 1) * kRing + kSink) * 4; }
+
+// Constant 100 MHz clock, read and waited for in one statement: a compiler-visible s_memrealtime
+// in a slow path can leave its SMEM result "pending" at the join with the fast path, and the
+// waitcnt pass then puts an s_waitcnt lgkmcnt(0) into every body that reads the reused SGPRs.
+__device__ __forceinline__ uint64_t now_ticks()
+{
+    uint64_t t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t));
+    return t;
+}
 
 // Bounded-spin helper, called every few polls: false (and the abort word raised) after the
 // timeout, or as soon as another wave has given up.
 __device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int lane)
 {
     // 100 MHz constant clock
-    const bool late = __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks;
+    const bool late = now_ticks() - t0 > a.timeout_ticks;
     if (late && lane == 0) __hip_atomic_store(&a.ctrl->abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int aborted = uniform((int)__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     return !(aborted || late);
@@ -263,6 +282,39 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
     }
 }
 
+// Register state of the hand-scheduled steady steps (R = 1, kArr8; sa_fill_steps.inc, generated by
+// tools/gen_fill_asm.py): Q / Qn / diag rotate roles every step, F alternates with F2.
+struct StepRegs {
+    int Q, Qn, diag, F, F2;
+    uint32_t acc0, acc1, acc2;
+    int bm;      // local: running max of (H << kb) - q over the body
+    int T[4];    // text-profile words of the body (4 steps each)
+    int g, kb;
+    int pfaddr, pf;  // HP: LDS address of this lane's next feed slot, and the value read there
+    int pubaddr, pubtag;  // HN: this lane's publish address and the body's lap tag
+    template <int K>
+    __device__ __forceinline__ void rotate()
+    {
+        if constexpr (K == 1)
+        {
+            const int a = Q;
+            Q = Qn;
+            Qn = diag;
+            diag = a;
+        }
+        else if constexpr (K == 2)
+        {
+            const int a = Q;
+            Q = diag;
+            diag = Qn;
+            Qn = a;
+        }
+    }
+};
+template <bool LOCAL, bool HN, bool HP>
+__device__ __forceinline__ void steps_asm(StepRegs &r);
+#include "sa_fill_steps.inc"
+
 // One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
@@ -315,10 +367,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
     lds_int *consIn = (lds_int *)&H.cons[w];
     lds_int *consOut = (lds_int *)&H.cons[w + 1];
-    // publishing lanes (64-U..63) and their column offset; the others write their own dummy slot
-    const bool pubLane = lane >= kWave - U;
-    const int pubRel = lane - (kWave - U);
-    lds_int *pubDummy = (lds_int *)&H.dummy[w][lane];
+    // publish target of this lane at ring offset 0: lanes 64-U..63 their column's slot, the others
+    // the sink (rings + (W+1) * kRing, shared by the waves: its contents are never read)
+    lds_int *pubBase = lane >= kWave - U ? rout + (lane - (kWave - U)) : rings + (H.nwaves + 1) * kRing + lane;
     // the strip's direction chunks (uniform base) and this lane's byte offset in a chunk
     uint32_t *mbase = a.masks + sd.mask_off * 4;
     const uint32_t moff = (uint32_t)(lane * Cfg<R>::LW * 4);
@@ -368,6 +419,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     // The read is checked at the boundary by the entries' tags (ring_tag); a slot not yet written
     // sends the wave to the slow path, which re-reads until every needed lane is there.
     int pfVal = 0;
+    int consDone = 0;    // last consumption word written
+    // address of this lane's feed slot for the body starting at step base (column base+1+lane)
+    auto feed_addr = [&](int base) __attribute__((always_inline)) { return rin + ring_slot(base + 1 + lane); };
     auto prefetch = [&](int base) __attribute__((always_inline)) {
         if constexpr (HP)
         {
@@ -395,30 +449,38 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             int x = pfVal ^ tag;
             if (__builtin_expect((ballot(x < 0) & need) != 0, 0))
             {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                const uint64_t t0 = now_ticks();
                 for (uint32_t spin = 1;; ++spin)
                 {
                     __builtin_amdgcn_s_sleep(1);
-                    x = ds_read_sync(rin + ring_slot(base + 1 + lane)) ^ tag;
+                    x = ds_read_sync(feed_addr(base)) ^ tag;
                     if ((ballot(x < 0) & need) == 0) break;
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
                 }
             }
             Q = x;  // lanes >= cnt: don't care
-            const int upto = base + U;
-            if (((upto & (kConsEvery - 1)) == 0) && lane == 0) lds_st(consIn, upto);
         }
     };
+    // consumption word for the strip above (its backpressure), at most every kConsEvery columns
+    auto consumed = [&](int upto) __attribute__((always_inline)) {
+        if constexpr (HP)
+            if (upto - consDone >= kConsEvery)
+            {
+                consDone = upto;
+                // (asm: no LDS operation of the compiler's may stay in flight into the next body)
+                if (lane == 0) ds_write_async(consIn, upto);
+            }
+    };
     // lanes 64-U..63 of Q hold the bottom row of columns s0-63 .. s0-64+U: one ds_write_b32 by every
-    // lane (the others to their dummy slot), tagged, after making sure the consumer has read the
-    // slots' previous lap
-    auto publish = [&](int s0) __attribute__((always_inline)) {
+    // lane (the others into the sink), tagged, after making sure the consumer has read the slots'
+    // previous lap
+    auto pub_wait = [&](int s0) __attribute__((always_inline)) {
         if constexpr (HN)
         {
             const int cLast = s0 - 64 + U;
             if (__builtin_expect(cLast - kRing > consKnown, 0))
             {
-                const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                const uint64_t t0 = now_ticks();
                 for (uint32_t spin = 1;; ++spin)
                 {
                     consKnown = uniform(lds_ld(consOut));
@@ -427,27 +489,73 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
                 }
             }
-            lds_int *dst = pubLane ? rout + ((s0 + pubRel) & kRingMask) : pubDummy;
-            lds_st(dst, Q | ring_tag(s0 - 63));
         }
     };
-    const uint64_t tStart = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto publish = [&](int s0) __attribute__((always_inline)) {
+        if constexpr (HN)
+        {
+            pub_wait(s0);
+            lds_st(pubBase + (s0 & kRingMask), Q | ring_tag(s0 - 63));
+        }
+    };
+    const uint64_t tStart = a.timeline ? now_ticks() : 0;
     load_codes(0, TA);
     if constexpr (kAhead == 2) load_codes(U, TB);
     prefetch(0);
     feed(0);
-    const uint64_t tFed = a.timeline ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t tFed = a.timeline ? now_ticks() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
     constexpr int kPfLead = U >= 8 ? U / 4 : 1;  // steps between the feed read and its use
-    auto body = [&](auto kind, auto second, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
+    // steady R = 1 bodies with int8 text profiles run hand-scheduled asm steps (sa_fill_steps.inc)
+    constexpr bool kAsm = R == 1 && SK == kArr8 && SA_FILL_ASM;
+    // pos: the body's place in its loop trip (0..3 in quads, 0..1 in pairs): odd bodies store the
+    // direction chunk (two bodies per chunk for R = 1), the trip's last one writes the consumption word
+    auto body = [&](auto kind, auto pos, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
         constexpr int KIND = decltype(kind)::value;
+        constexpr int POS = decltype(pos)::value;
+        using second = std::integral_constant<bool, (POS & 1) == 1>;
         const int s1 = s0 + U;
         load_codes(s0 + kAhead * U, Tn);
-        run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
-        prefetch(s1);
-        run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
-        if constexpr (Cfg<R>::BPC == 1 || decltype(second)::value)
+        if constexpr (kAsm && KIND == kSteady)
+        {
+            static_assert(U == 16 && kPfLead == 4 && NT == 4, "sa_fill_steps.inc is generated for these");
+            StepRegs r;
+            r.Q = Q;
+            r.diag = upPrev;
+            r.F = F[0];
+            r.acc0 = acc[0][0];
+            r.acc1 = acc[1][0];
+            r.acc2 = acc[2][0];
+            r.bm = -16;  // below every (H << kb) - q
+            sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
+            r.g = g;
+            r.kb = kb;
+            r.pfaddr = HP ? (int)lds_off(feed_addr(s1)) : 0;
+            pub_wait(s0);  // the block ends with the publish write (HN)
+            r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
+            r.pubtag = ring_tag(s0 - 63);
+            steps_asm<LOCAL, HN, HP>(r);  // with HP: reads the next body's feed after step 12
+            pfVal = r.pf;
+            Q = r.Q;
+            upPrev = r.diag;
+            F[0] = r.F;
+            acc[0][0] = r.acc0;
+            acc[1][0] = r.acc1;
+            if constexpr (LOCAL)
+            {
+                acc[2][0] = r.acc2;
+                const int kmask = (1 << kb) - 1;
+                best[0] = max(best[0], r.bm + (kmask - (s0 & kmask)));
+            }
+        }
+        else
+        {
+            run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+            prefetch(s1);
+            run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+        }
+        if constexpr (Cfg<R>::BPC == 1 || second::value)
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
             store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);
@@ -477,14 +585,17 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 });
             }
         }
-        publish(s0);
+        if constexpr (!(kAsm && KIND == kSteady)) publish(s0);
         feed(s1);
+        if constexpr (POS == (kAhead == 2 ? 3 : 1)) consumed(s1 + U);
     };
     using KSteady = std::integral_constant<int, kSteady>;
     using KStart = std::integral_constant<int, kStart>;
     using KGeneric = std::integral_constant<int, kGeneric>;
-    using First = std::false_type;
-    using Second = std::true_type;
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
     // tail pairs: from the first pair holding a body with s1 > n (only where the final state is read)
     const int sTail = needFinal ? max(0, (n - 2 * U + 1 + 2 * U - 1) / (2 * U) * (2 * U)) : nSteps;
     int s0 = 0;
@@ -495,15 +606,15 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         auto phase = [&](auto kind, int end) __attribute__((always_inline)) {
             for (; s0 + 2 * U < end; s0 += 4 * U)
             {
-                body(kind, First{}, s0, TA, TC);
-                body(kind, Second{}, s0 + U, TB, TD);
-                body(kind, First{}, s0 + 2 * U, TC, TA);
-                body(kind, Second{}, s0 + 3 * U, TD, TB);
+                body(kind, P0{}, s0, TA, TC);
+                body(kind, P1{}, s0 + U, TB, TD);
+                body(kind, P2{}, s0 + 2 * U, TC, TA);
+                body(kind, P3{}, s0 + 3 * U, TD, TB);
             }
             if (s0 < end)
             {
-                body(kind, First{}, s0, TA, TC);
-                body(kind, Second{}, s0 + U, TB, TD);
+                body(kind, P2{}, s0, TA, TC);
+                body(kind, P3{}, s0 + U, TB, TD);
                 s0 += 2 * U;
                 sfor<NT>([&](auto Qc) {
                     constexpr int q = decltype(Qc)::value;
@@ -521,18 +632,18 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         if constexpr (!kIsArr<SK>)
             for (; s0 < min(kWave, sTail); s0 += 2 * U)
             {
-                body(KStart{}, First{}, s0, TA, TB);
-                body(KStart{}, Second{}, s0 + U, TB, TA);
+                body(KStart{}, P0{}, s0, TA, TB);
+                body(KStart{}, P1{}, s0 + U, TB, TA);
             }
         for (; s0 < sTail; s0 += 2 * U)
         {
-            body(KSteady{}, First{}, s0, TA, TB);
-            body(KSteady{}, Second{}, s0 + U, TB, TA);
+            body(KSteady{}, P0{}, s0, TA, TB);
+            body(KSteady{}, P1{}, s0 + U, TB, TA);
         }
         for (; s0 < nSteps; s0 += 2 * U)
         {
-            body(KGeneric{}, First{}, s0, TA, TB);
-            body(KGeneric{}, Second{}, s0 + U, TB, TA);
+            body(KGeneric{}, P0{}, s0, TA, TB);
+            body(KGeneric{}, P1{}, s0 + U, TB, TA);
         }
     }
     if (a.timeline && lane == 0)
@@ -540,7 +651,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         uint64_t *tl = a.timeline + kTimelineWords * (size_t)idx;
         tl[0] = tStart;
         tl[1] = tFed;
-        tl[2] = __builtin_amdgcn_s_memrealtime();
+        tl[2] = now_ticks();
         tl[4] = cFed;  // shader clock (s_memtime): effective frequency = clocks / real time
         tl[5] = __builtin_amdgcn_s_memtime();
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
@@ -738,7 +849,7 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
 
 // One wave per two strips (pairs sA, sA+1); 4 waves per workgroup; dynamic queue over strip pairs.
 template <int R>
-__global__ __launch_bounds__(kWave * kMaxWaves, 2) void fill_pair_kernel(FillArgs a)
+__global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillArgs a)
 {
     __shared__ int unit;
     const int lane = threadIdx.x & (kWave - 1);
@@ -782,7 +893,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
     // slots of columns -63..0 are never copied in: give them their lap-0 tag, or the zeroed entries
     // would pass for lap-1 columns 1985..2048 (a compute-wave producer publishes from column -63)
     if (nIn > 0) lds_st(r0 + ring_slot(lane - 63), ring_tag(lane - 63));
-    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t0 = now_ticks();
     for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
     {
         bool moved = false;
@@ -793,17 +904,18 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
             const int want = min(min(kWave, nIn - copied), room);
             if (want >= min(16, nIn - copied))
             {
-                uint64_t probe = 0;
-                if (lane == 0) probe = load_granule(bin + copied + min(want, 16) - 1);
-                if ((uint32_t)uniform((int)(uint32_t)(probe >> 32)) == a.epoch)
+                // every poll loads the whole window (one round trip from the producer's store to
+                // the ring; a lane-0 probe first would add a second): 512 bytes per poll per waiting
+                // group is nothing next to the fill's own traffic
+                const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
+                const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
+                const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
+                if (cnt >= min(16, nIn - copied))
                 {
-                    const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
-                    const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
-                    const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
                     const int c = copied + lane + 1;
                     if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
                     copied += cnt;
-                    moved = cnt > 0;
+                    moved = true;
                 }
             }
         }
@@ -823,7 +935,7 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
         }
         if (moved)
         {
-            t0 = __builtin_amdgcn_s_memrealtime();
+            t0 = now_ticks();
             continue;
         }
         for (int z = 0; z < a.io_sleep; ++z) __builtin_amdgcn_s_sleep(1);
@@ -860,6 +972,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         {
             const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
             H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
+            H.nwaves = W;
         }
         if (threadIdx.x <= kMaxWaves) H.cons[threadIdx.x] = 0;
         if constexpr (CHAIN)
