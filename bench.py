@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=["headline", "local", "batch", "dna8k", "protein4k"], default="headline")
     ap.add_argument("--size", type=int, default=32768)
+    ap.add_argument("--pattern-len", type=int, default=0, help="headline/local: rows (default: --size)")
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
@@ -219,6 +220,7 @@ def main():
                     "gap": gap, "parallelism": f"replicas{world}"}
     elif args.workload in ("headline", "local"):
         n = m = args.size
+        m = args.pattern_len or n
         mode = 0 if args.workload == "headline" else 1
         t = synthetic.random_sequence(6 + 1000 * rank, n, 4)
         p = synthetic.random_sequence(7 + 1000 * rank, m, 4)

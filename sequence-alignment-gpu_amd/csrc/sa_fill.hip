@@ -75,21 +75,24 @@ __device__ __forceinline__ int ds_read_sync(const lds_int *p)
 }
 constexpr int kRing = 2048;        // ring entries (columns), power of two
 constexpr int kRingMask = kRing - 1;
-#ifndef SA_CODE_AHEAD
-#define SA_CODE_AHEAD 2  // R = 1 text-code loads run this many bodies ahead (1 or 2)
-#endif
-#ifndef SA_PF_FIRST
-#define SA_PF_FIRST 1  // body boundary order: feed check, prefetch, publish, consumption word
-#endif
-#ifndef SA_ABL
-#define SA_ABL 0  // timing ablations of the hand-off (development builds only; results are wrong)
+// Tuning constants of the shipped build. Development builds (tools/build_exp.sh defines
+// SA_EXPERIMENT) may override the ones below and enable timing ablations (SA_EXP_*: results wrong by
+// design); the shipped build refuses any override, so a stray -D cannot change what it computes.
+#ifdef SA_EXPERIMENT
+#ifndef SA_PF_LEAD
+#define SA_PF_LEAD 4
 #endif
 #ifndef SA_FILL_ASM
-#define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body, for A/B)
+#define SA_FILL_ASM 1
 #endif
-#ifndef SA_CODE_AHEAD_LOCAL
-#define SA_CODE_AHEAD_LOCAL 2
+#else
+#if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE)
+#error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
+#define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
+#define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
+#endif
+constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
@@ -395,13 +398,18 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     });
     int upPrev = 0, Q = 0;
     // text codes, double-buffered across the two bodies of a pair (no register copies)
-    // text codes: SA_CODE_AHEAD = 1 double-buffers across the two bodies of a pair; 2 keeps four
-    // buffers and loads every body's codes two bodies ahead (bodies run in quads)
-    constexpr int kAhead = R != 1 ? 1 : LOCAL ? SA_CODE_AHEAD_LOCAL : SA_CODE_AHEAD;  // taller strips: long bodies
+    // text codes: R = 1 keeps four buffers and loads every body's codes two bodies ahead (bodies run
+    // in quads; with one body of look-ahead a lone strip took 54.6 clk/step instead of 42: the first
+    // touch of a code line misses L2); taller strips double-buffer across the two bodies of a pair
+    constexpr int kAhead = R != 1 ? 1 : kCodeAhead;
     int TA[NT], TB[NT], TC[NT], TD[NT];
     auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_CODES_CONST)
+        const uint32_t off = coff + (uint32_t)(s0 & 63);  // timing ablation: results are wrong
+#else
         const uint32_t off = coff + (uint32_t)(SK == kArr8 ? s0 : s0 * 4);
+#endif
         sfor<NT / 4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value * 4;
             const i32x4u v = *(const i32x4u *)(cbase + off + q * 4);
@@ -449,13 +457,20 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             int x = pfVal ^ tag;
             if (__builtin_expect((ballot(x < 0) & need) != 0, 0))
             {
-                const uint64_t t0 = now_ticks();
+                // a chained strip is paced by the strip above and often arrives a little early:
+                // re-read at once for a while (this wave is alone on its SIMD), sleep only when the
+                // wait is long (the strip's start); the give-up clock starts after 256 polls
+                uint64_t t0 = 0;
                 for (uint32_t spin = 1;; ++spin)
                 {
-                    __builtin_amdgcn_s_sleep(1);
+                    if (spin > 16) __builtin_amdgcn_s_sleep(1);
                     x = ds_read_sync(feed_addr(base)) ^ tag;
                     if ((ballot(x < 0) & need) == 0) break;
-                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+                    if ((spin & 255) == 0)
+                    {
+                        if (t0 == 0) t0 = now_ticks();
+                        else if (!keep_waiting(a, t0, lane)) break;
+                    }
                 }
             }
             Q = x;  // lanes >= cnt: don't care
@@ -506,7 +521,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     const uint64_t tFed = a.timeline ? now_ticks() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
-    constexpr int kPfLead = U >= 8 ? U / 4 : 1;  // steps between the feed read and its use
+    constexpr int kPfLead = U >= 8 ? SA_PF_LEAD * U / 16 : 1;  // steps between the feed read and its use
     // steady R = 1 bodies with int8 text profiles run hand-scheduled asm steps (sa_fill_steps.inc)
     constexpr bool kAsm = R == 1 && SK == kArr8 && SA_FILL_ASM;
     // pos: the body's place in its loop trip (0..3 in quads, 0..1 in pairs): odd bodies store the
@@ -519,7 +534,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         load_codes(s0 + kAhead * U, Tn);
         if constexpr (kAsm && KIND == kSteady)
         {
-            static_assert(U == 16 && kPfLead == 4 && NT == 4, "sa_fill_steps.inc is generated for these");
+            static_assert(U == 16 && NT == 4, "sa_fill_steps.inc is generated for these");
             StepRegs r;
             r.Q = Q;
             r.diag = upPrev;
@@ -555,7 +570,11 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             prefetch(s1);
             run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
         }
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STORE)
+        if constexpr (false)  // timing ablation: no direction planes are written
+#else
         if constexpr (Cfg<R>::BPC == 1 || second::value)
+#endif
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
             store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);

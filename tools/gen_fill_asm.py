@@ -33,7 +33,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "sequence-alignment-gpu_amd", "csrc", "sa_fill_steps.inc")
 
 U = 16
-PF_STEP = 12  # with a strip above, the next body's feed read is issued after this step (kPfLead = 4)
+# with a strip above, the next body's feed read is issued after this step (kPfLead = U - PF_STEP)
+PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "12"))
 
 
 def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
