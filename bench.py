@@ -177,11 +177,9 @@ class Chunked:
         if two:
             self.s_fill.wait_stream(self.s_tb)
 
-    def results(self) -> list[dict]:
-        out = []
-        for j in self.jobs:
-            out += j.plan.results(self.s_fill.cuda_stream)
-        return out
+    def results(self) -> np.ndarray:
+        """Every pair's sa_result (numpy structured array; one copy per plan, no per-pair objects)."""
+        return np.concatenate([j.plan.results_array(self.s_fill.cuda_stream) for j in self.jobs])
 
 
 def main():
@@ -264,7 +262,7 @@ def main():
             job.fill_and_traceback(ev)
             r = job.results()
             if world > 1:
-                distributed.gather_results(r, npairs, world, rank, dev)
+                distributed.gather_array(r, npairs, world, rank, dev)
         else:
             job.fill(ev)
 
@@ -301,15 +299,15 @@ def main():
     fill_ms_e2e, tb_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
 
     tmax = elapsed
-    scores = [r["score"] for r in res]
+    scores = [int(x) for x in res["score"]]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tmax = float(tt.item())
         if args.workload == "batch":
-            allres = distributed.gather_results(res, npairs, world, rank, dev)
+            allres = distributed.gather_array(res, npairs, world, rank, dev)
             if rank == 0:
-                scores = [r["score"] for r in allres]
+                scores = allres[:, 0].tolist()
     cells_total = cells_rank * world
     value = cells_total * args.steps / tmax / 1e9
     if rank == 0:

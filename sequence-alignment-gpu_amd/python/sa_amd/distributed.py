@@ -14,17 +14,50 @@ def shard(num_pairs: int, world: int, rank: int) -> list[int]:
     return list(range(rank, num_pairs, world))
 
 
-def gather_results(results: list[dict], num_pairs: int, world: int, rank: int, device) -> list[dict] | None:
+def _as_rows(results) -> "np.ndarray":
+    """(k, 4) int64 rows of FIELDS from a list of result dicts or a numpy structured array
+    (engine.RESULT_DTYPE); uint64 starts such as (uint64)-1 keep their bits."""
+    import numpy as np
+    if isinstance(results, np.ndarray):
+        return np.stack([results[f].astype(np.uint64).view(np.int64) for f in FIELDS], axis=1) if len(results) \
+            else np.zeros((0, len(FIELDS)), np.int64)
+    to_i64 = lambda v: int(v) - (1 << 64) if int(v) >= (1 << 63) else int(v)
+    return np.array([[to_i64(r[f]) for f in FIELDS] for r in results], dtype=np.int64).reshape(-1, len(FIELDS))
+
+
+def gather_array(results, num_pairs: int, world: int, rank: int, device):
+    """Gathers every rank's per-pair result rows to rank 0: an (num_pairs, 4) int64 array of FIELDS in
+    global pair order on rank 0 (uint64 starts as their int64 bit patterns), None elsewhere."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    width = (num_pairs + world - 1) // world
+    rows = _as_rows(results)
+    buf = torch.full((width, len(FIELDS)), -1, dtype=torch.int64, device=device)
+    if len(rows):
+        buf[: len(rows)] = torch.from_numpy(rows).to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    out = np.empty((num_pairs, len(FIELDS)), np.int64)
+    for r, part in enumerate(parts):
+        idx = shard(num_pairs, world, r)
+        out[idx] = part.cpu().numpy()[: len(idx)]
+    return out
+
+
+def gather_results(results, num_pairs: int, world: int, rank: int, device) -> list[dict] | None:
     """Gathers every rank's per-pair results to rank 0 in global pair order; None on other ranks."""
     import torch
     import torch.distributed as dist
 
     width = (num_pairs + world - 1) // world
     buf = torch.full((width, len(FIELDS)), -1, dtype=torch.int64, device=device)
-    if results:
-        to_i64 = lambda v: int(v) - (1 << 64) if int(v) >= (1 << 63) else int(v)  # uint64 starts, e.g. (uint64)-1
-        vals = [[to_i64(r[f]) for f in FIELDS] for r in results]
-        buf[: len(results)] = torch.tensor(vals, dtype=torch.int64, device=device)
+    rows = _as_rows(results)
+    if len(rows):
+        buf[: len(rows)] = torch.from_numpy(rows).to(device)
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
     dist.gather(buf, parts, dst=0)
     if rank != 0:

@@ -64,7 +64,7 @@ def _load():
     L.sa_plan_destroy.argtypes = [P]
     L.sa_plan_fill.argtypes = [P, P, P, P]
     L.sa_plan_traceback.argtypes = [P, P]
-    L.sa_plan_fetch_results.argtypes = [P, ctypes.POINTER(SaResult), P]
+    L.sa_plan_fetch_results.argtypes = [P, P, P]
     L.sa_plan_fetch_alignment.argtypes = [P, ctypes.c_int64, P, P, U64, P]
     L.sa_plan_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(U64), ctypes.POINTER(U64)]
@@ -125,6 +125,12 @@ def align_pair(mode: int, text: np.ndarray, pattern: np.ndarray, S: np.ndarray, 
     L = res.num_alignment_bytes
     return {"score": res.score, "num_bytes": L, "start_text": res.start_text, "start_pattern": res.start_pattern,
             "aligned_text": at.raw[:L].decode(), "aligned_pattern": ap.raw[:L].decode(), "fill_us": fill_us.value}
+
+
+# numpy view of sa_result (include/sa_hip.h): int32 score, int32 status, uint64 x 3
+RESULT_DTYPE = np.dtype([("score", "<i4"), ("status", "<i4"), ("num_bytes", "<u8"), ("start_text", "<u8"),
+                         ("start_pattern", "<u8")])
+assert RESULT_DTYPE.itemsize == ctypes.sizeof(SaResult)
 
 
 class SaHostPair(ctypes.Structure):
@@ -203,6 +209,12 @@ class Plan:
         _check(lib.sa_plan_fetch_results(self.handle, out, stream))
         return [{"score": r.score, "num_bytes": r.num_alignment_bytes, "start_text": r.start_text,
                  "start_pattern": r.start_pattern} for r in out[: self.num_pairs]]
+
+    def results_array(self, stream: int | None = None) -> np.ndarray:
+        """Every pair's sa_result as one numpy structured array (RESULT_DTYPE): no per-pair objects."""
+        out = np.empty(max(1, self.num_pairs), RESULT_DTYPE)
+        _check(lib.sa_plan_fetch_results(self.handle, out.ctypes.data, stream))
+        return out[: self.num_pairs]
 
     def directions(self, index: int, stream: int | None = None) -> np.ndarray:
         """Decoded (m+1)x(n+1) DIRECTION matrix of pair `index` (reference layout, for verification)."""

@@ -81,3 +81,46 @@ def test_sharded_batch_gather_world2(mode):
         assert got[i] == {k: r[k] for k in distributed.FIELDS}, i
     # the deal is round-robin and covers every pair exactly once
     assert sorted(distributed.shard(num, 2, 0) + distributed.shard(num, 2, 1)) == list(range(num))
+
+
+def _array_worker(rank, world, port, num, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+    import numpy as np
+    import torch.distributed as dist
+
+    from sa_amd import distributed
+    from sa_amd.engine import RESULT_DTYPE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = distributed.shard(num, world, rank)
+    arr = np.zeros(len(mine), RESULT_DTYPE)
+    arr["score"] = [10 * i - 7 for i in mine]
+    arr["num_bytes"] = [i + 3 for i in mine]
+    arr["start_text"] = [(1 << 64) - 1 if i % 3 == 0 else i for i in mine]
+    arr["start_pattern"] = [i * 5 for i in mine]
+    out = distributed.gather_array(arr, num, world, rank, "cpu")
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_gather_array_world2():
+    """The bench's vectorized result path: structured sa_result arrays -> rank 0, uint64 bits kept."""
+    import numpy as np
+    num = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_array_worker, args=(r, 2, port, num, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got.shape == (num, 4)
+    for i in range(num):
+        st = -1 if i % 3 == 0 else i  # (uint64)-1 as its int64 bit pattern
+        assert got[i].tolist() == [10 * i - 7, i + 3, st, i * 5], i
+    assert np.uint64(got[0, 2].view(np.uint64)) == np.uint64((1 << 64) - 1)
