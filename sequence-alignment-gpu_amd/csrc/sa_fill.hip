@@ -86,7 +86,8 @@ constexpr int kRingMask = kRing - 1;
 #define SA_FILL_ASM 1
 #endif
 #else
-#if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE)
+#if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
+    defined(SA_EXP_NO_FEED_WAIT)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -295,6 +296,8 @@ struct StepRegs {
     int g, kb;
     int pfaddr, pf;  // HP: LDS address of this lane's next feed slot, and the value read there
     int pubaddr, pubtag;  // HN: this lane's publish address and the body's lap tag
+    int ctag;             // HP: lap tag the feed entries must carry
+    uint64_t bad;         // HP: lanes whose feed entry did not carry it
     template <int K>
     __device__ __forceinline__ void rotate()
     {
@@ -427,6 +430,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     // The read is checked at the boundary by the entries' tags (ring_tag); a slot not yet written
     // sends the wave to the slow path, which re-reads until every needed lane is there.
     int pfVal = 0;
+    bool pfTagged = false;  // pfVal already XORed with its tag by the asm body, bad lanes in pfBad
+    uint64_t pfBad = 0;
     int consDone = 0;    // last consumption word written
     // address of this lane's feed slot for the body starting at step base (column base+1+lane)
     auto feed_addr = [&](int base) __attribute__((always_inline)) { return rin + ring_slot(base + 1 + lane); };
@@ -450,12 +455,25 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         }
         else
         {
-            // lanes 0..cnt-1 carry columns base+1 .. base+cnt <= n; one aligned run: one tag
+            // lanes 0..cnt-1 carry columns base+1 .. base+cnt <= n; one aligned run: one tag. The asm
+            // bodies have applied the tag already (pfTagged) and left the bad-lane mask in pfBad.
             const int tag = ring_tag(base + 1);
-            const int cnt = min(max(n - base, 0), U);
-            const uint64_t need = (1ull << cnt) - 1;
-            int x = pfVal ^ tag;
-            if (__builtin_expect((ballot(x < 0) & need) != 0, 0))
+            // need = (1 << clamp(n - base, 0, U)) - 1, as four SALU ops (left to itself the compiler
+            // clamps in VALU and round-trips through v_readfirstlane)
+            uint64_t need;
+            int cnt;
+            asm("s_sub_i32 %1, %2, %3\n\ts_max_i32 %1, %1, 0\n\ts_min_i32 %1, %1, %4\n\ts_bfm_b64 %0, %1, 0"
+                : "=s"(need), "=&s"(cnt)
+                : "s"(n), "s"(base), "i"(U)
+                : "scc");
+            int x = pfTagged ? pfVal : pfVal ^ tag;
+            const uint64_t bad = pfTagged ? pfBad : ballot(x < 0);
+            pfTagged = false;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_FEED_WAIT)
+            if (base > 0 && false)  // timing ablation: never waits after the first feed (results wrong)
+#else
+            if (__builtin_expect((bad & need) != 0, 0))
+#endif
             {
                 // a chained strip is paced by the strip above and often arrives a little early:
                 // re-read at once for a while (this wave is alone on its SIMD), sleep only when the
@@ -547,11 +565,17 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             r.g = g;
             r.kb = kb;
             r.pfaddr = HP ? (int)lds_off(feed_addr(s1)) : 0;
+            r.ctag = ring_tag(s1 + 1);
             pub_wait(s0);  // the block ends with the publish write (HN)
             r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
             r.pubtag = ring_tag(s0 - 63);
             steps_asm<LOCAL, HN, HP>(r);  // with HP: reads the next body's feed after step 12
-            pfVal = r.pf;
+            if constexpr (HP)
+            {
+                pfVal = r.pf;
+                pfBad = r.bad;
+                pfTagged = true;
+            }
             Q = r.Q;
             upPrev = r.diag;
             F[0] = r.F;

@@ -43,11 +43,12 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     FA, FB = "%3", "%4"
     D, M, T0, T1 = "%5", "%6", "%7", "%8"
     ACC0, ACC1 = "%9", "%10"
-    # outputs first (Q .. acc1 = %0..%10, local extras %11..%15, then the feed value), then inputs
-    # (T words, local g / kb, feed address, publish address and tag)
-    h = 1 if hp else 0
+    # outputs first (Q .. acc1 = %0..%10, local extras %11..%15, then the feed value and its
+    # bad-lane mask), then inputs (T words, local g / kb, feed address and tag, publish address and tag)
+    h = 2 if hp else 0
     nout = (11 if not local else 16) + h
-    PF = f"%{nout - 1}"
+    PF = f"%{nout - 2}"
+    BAD = f"%{nout - 1}"
     TW = [f"%{nout + i}" for i in range(4)]
     k = nout + 4
     ACC2 = BM = X = T2 = KEY = G = KB = None
@@ -55,9 +56,9 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
         ACC2, BM, X, T2, KEY = "%11", "%12", "%13", "%14", "%15"
         G, KB = f"%{k}", f"%{k + 1}"
         k += 2
-    PFA = f"%{k}"
+    PFA, CTAG = f"%{k}", f"%{k + 1}"
     if hp:
-        k += 1
+        k += 2
     PADDR, PTAG = f"%{k}", f"%{k + 1}"
     roles = [A, B, C]
     fregs = [FA, FB]
@@ -102,6 +103,10 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
         roles = [b, c, a]
     if hp:
         out.append("s_waitcnt lgkmcnt(0)")  # the feed read (issued 4 steps ago) is there
+        # tag check: x = entry ^ expected tag (the value when it matches), bad lanes = x < 0; the
+        # publish below stands between the compare and the caller's SALU test of its mask
+        out.append(f"v_xor_b32_e32 {PF}, {CTAG}, {PF}")
+        out.append(f"v_cmp_gt_i32_e64 {BAD}, 0, {PF}")
     if hn:
         # publish: lanes 48..63 of the accumulated Q (now role B) with the body's lap tag; the write
         # stays in flight past the block (the compiler sees no LDS operation it would wait for)
@@ -139,12 +144,12 @@ def main():
                 if local:
                     lines.append("          , \"+v\"(r.acc2), \"+v\"(r.bm), \"=&v\"(X), \"=&v\"(t2), \"=&v\"(key)")
                 if hp:
-                    lines.append("          , \"=&v\"(r.pf)")
+                    lines.append("          , \"=&v\"(r.pf), \"=s\"(r.bad)")
                 ins = "\"v\"(r.T[0]), \"v\"(r.T[1]), \"v\"(r.T[2]), \"v\"(r.T[3])"
                 if local:
                     ins += ", \"s\"(r.g), \"s\"(r.kb)"
                 if hp:
-                    ins += ", \"v\"(r.pfaddr)"
+                    ins += ", \"v\"(r.pfaddr), \"s\"(r.ctag)"
                 if hn:
                     ins += ", \"v\"(r.pubaddr), \"s\"(r.pubtag)"
                 lines.append(f"        : {ins});")
