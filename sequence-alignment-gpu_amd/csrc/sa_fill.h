@@ -36,7 +36,7 @@ struct FillArgs {
                                 // than half a CU's LDS keeps one workgroup per CU)
 };
 
-constexpr int kTimelineWords = 6;  // SA_TIMELINE record per strip
+constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip (words 6..35: experiment progress stamps)
 constexpr int kMaxWaves = 4;       // compute waves per chain workgroup (+1 I/O wave: 320 threads; one
                                    // compute wave per SIMD: two per SIMD ran 2.2x slower per step)
 constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed batch kernel

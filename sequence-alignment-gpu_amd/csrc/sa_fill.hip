@@ -387,10 +387,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     });
     const int nSteps = sd.nsteps;  // a multiple of 2U
     // Lanes must stop at column n (kGeneric bodies at the end) where the final state is read: the
-    // global score H(m, n) in the strip holding row m, and the local best-cell keys (a garbage key
-    // past column n could shadow a real one of the same key block). Other strips run their tail
-    // unmasked.
-    const bool needFinal = LOCAL || (m - sd.row0 >= 0 && m - sd.row0 < kWave * R);
+    // global score H(m, n) in the strip holding row m, and the local best-cell keys when a garbage
+    // key past column n could shadow a real one of the same key block. Other strips run their tail
+    // unmasked. Local strips with text profiles and g > 0 need no masked tail: past column n the
+    // profile holds zeros (S + g = 0), so a cell there has H <= max(its neighbours' H) - g, every
+    // key past n is below the pair's best H, and the fold discards it by column. (The masked tail
+    // mattered: strip k+1 ends only after strip k's tail, so slow tails set the chain's end cadence
+    // and stretched every strip behind them, 3.34 -> DESIGN.md §3.1.)
+    const bool needFinal = LOCAL ? !(kIsArr<SK> && g > 0) : (m - sd.row0 >= 0 && m - sd.row0 < kWave * R);
 
     // column-0 boundary: global F(i,0) = 0; local H(i,0) = 0
     int F[R], best[R];
@@ -423,6 +427,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         });
     };
     int consKnown = 0;   // columns the consumer of rout is known to have read
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+    uint32_t dbgFeedSlow = 0, dbgFeedSpins = 0, dbgPubSlow = 0, dbgPubSpins = 0;  // slow-path counts
+#endif
     // Feed values for the body starting at step base (columns base+1 .. base+U, lanes 0..U-1 of Q)
     // are read kPfLead steps before that body starts, in the middle of the previous body: early
     // enough to cover the LDS latency, late enough that the strip above has published them by then
@@ -479,8 +486,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 // re-read at once for a while (this wave is alone on its SIMD), sleep only when the
                 // wait is long (the strip's start); the give-up clock starts after 256 polls
                 uint64_t t0 = 0;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                ++dbgFeedSlow;
+#endif
                 for (uint32_t spin = 1;; ++spin)
                 {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                    ++dbgFeedSpins;
+#endif
                     if (spin > 16) __builtin_amdgcn_s_sleep(1);
                     x = ds_read_sync(feed_addr(base)) ^ tag;
                     if ((ballot(x < 0) & need) == 0) break;
@@ -514,8 +527,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             if (__builtin_expect(cLast - kRing > consKnown, 0))
             {
                 const uint64_t t0 = now_ticks();
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                ++dbgPubSlow;
+#endif
                 for (uint32_t spin = 1;; ++spin)
                 {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                    ++dbgPubSpins;
+#endif
                     consKnown = uniform(lds_ld(consOut));
                     if (cLast - kRing <= consKnown) break;
                     __builtin_amdgcn_s_sleep(1);
@@ -549,6 +568,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         constexpr int POS = decltype(pos)::value;
         using second = std::integral_constant<bool, (POS & 1) == 1>;
         const int s1 = s0 + U;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+        // progress stamps every 4096 columns (timeline words 6..15)
+        if (a.timeline && (s0 & 4095) == 0 && (s0 >> 12) < 10 && lane == 0)
+        {
+            a.timeline[kTimelineWords * (size_t)idx + 6 + (s0 >> 12)] = now_ticks();
+            a.timeline[kTimelineWords * (size_t)idx + 26 + (s0 >> 12)] = __builtin_amdgcn_s_memtime();
+        }
+#endif
         load_codes(s0 + kAhead * U, Tn);
         if constexpr (kAsm && KIND == kSteady)
         {
@@ -696,6 +723,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         tl[1] = tFed;
         tl[2] = now_ticks();
         tl[4] = cFed;  // shader clock (s_memtime): effective frequency = clocks / real time
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+        tl[36] = dbgFeedSlow;
+        tl[37] = dbgFeedSpins;
+        tl[38] = dbgPubSlow;
+        tl[39] = dbgPubSpins;
+#endif
         tl[5] = __builtin_amdgcn_s_memtime();
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
         tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
@@ -957,6 +990,12 @@ __device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp,
                 {
                     const int c = copied + lane + 1;
                     if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                    // I/O progress stamps: when ring[0] got column 4096q (timeline words 16..25 of
+                    // the group's first strip)
+                    if (a.timeline && lane == 0 && ((copied + cnt) >> 12) != (copied >> 12) && ((copied + cnt) >> 12) < 10)
+                        a.timeline[kTimelineWords * (size_t)first + 16 + ((copied + cnt) >> 12)] = now_ticks();
+#endif
                     copied += cnt;
                     moved = true;
                 }
@@ -1056,6 +1095,14 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
             }
         }
     }
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_HOLD)
+    // experiment: finished workgroups stay resident (sleeping) until every workgroup has finished
+    if (threadIdx.x == 0)
+        while (__hip_atomic_load(&a.ctrl->queue_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               (unsigned)(a.num_groups + gridDim.x))
+            __builtin_amdgcn_s_sleep(127);
+    __syncthreads();
+#endif
 }
 
 // Fill launches, one translation unit per strip height R (fill_r<R>.hip instantiates

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--mode", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pairs", type=int, default=1, help="independent copies of the pair (contention test)")
+    ap.add_argument("--score", default="blast", help="blast (+5/-4) or MATCH,MISMATCH (e.g. 1,-3)")
     args = ap.parse_args()
     if args.waves:
         os.environ["SA_WAVES_PER_GROUP"] = str(args.waves)
@@ -46,6 +47,10 @@ def main():
     from sa_amd import synthetic
     from sa_amd.batch import DeviceBatch
     S = synthetic.blast_matrix()
+    if args.score != "blast":
+        mt, mm = (int(x) for x in args.score.split(","))
+        S = np.full((4, 4), mm, dtype=np.int32)
+        np.fill_diagonal(S, mt)
     t = synthetic.random_sequence(6, args.n, 4)
     p = synthetic.random_sequence(7, args.m, 4)
     b = DeviceBatch(args.mode, S, 5, [t] * args.pairs, [p] * args.pairs, rows_per_lane=args.R)
@@ -54,7 +59,9 @@ def main():
     b.fill()  # the file holds the last fill's timeline
     import torch
     torch.cuda.synchronize()
-    tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 6)
+    tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 48)
+    if os.environ.get("SA_TL_SAVE"):
+        np.save(os.environ["SA_TL_SAVE"], tl)  # raw records for offline analysis
     start, fed, end = (tl[:, i].astype(np.int64) for i in range(3))
     xcc = (tl[:, 3] >> 32).astype(np.int64)
     hw = (tl[:, 3] & 0xffffffff).astype(np.int64)
@@ -94,6 +101,33 @@ def main():
         "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
         "simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in hw[:8]],
     }
+    prog = tl[:, 6:16].astype(np.int64)
+    iop = tl[:, 16:26].astype(np.int64)
+    if prog[:, 1].any():
+        # experiment builds (SA_EXP_PROGRESS): time at columns 0, 4096, ... per strip; the lag between
+        # consecutive strips at each checkpoint shows whether a consumer falls behind its producer
+        ok = (prog > 0).all(axis=0)
+        pl = np.diff(prog[:, ok], axis=0) * 10.0
+        rec["progress_lag_ns_by_checkpoint"] = [round(float(x), 1) for x in pl.mean(axis=0)]
+        kk = np.arange(1, len(prog))
+        okr = (prog[1:, 1:9] > 0).all(axis=1) & (prog[:-1, 1:9] > 0).all(axis=1)
+        lagq = (prog[1:, 1:9] - prog[:-1, 1:9]) * 10.0  # ns, lag of strip k behind k-1 at checkpoints 1..8
+        for nm, sel in (("in_group", (kk % W) != 0), ("cross_group", (kk % W) == 0)):
+            L = lagq[sel & okr]
+            rec[f"lag_ns_by_checkpoint_{nm}"] = [round(float(x), 1) for x in L.mean(axis=0)]
+        rec["progress_lag_ns_first_strips"] = [[round(float(x), 1) for x in r] for r in pl[:6]]
+        seg = np.diff(prog[:, ok], axis=1) * 10.0 / 4096
+        rec["ns_per_step_by_segment_first"] = [round(float(x), 2) for x in seg[1]]
+        rec["ns_per_step_by_segment_last"] = [round(float(x), 2) for x in seg[-2]]
+        rec["ns_per_step_by_segment_every32"] = [[k] + [round(float(x), 1) for x in seg[k]] for k in range(0, len(seg), 32)]
+        # I/O wave: time ring[0] of group g got column 4096q minus the time the group's first strip
+        # reached column 4096q (negative: the feed was there first, the strip was the bottleneck)
+        gi = [k for k in range(W, len(prog), W) if iop[k, 1] > 0]
+        rec["io_ahead_us_every8groups"] = [[k] + [round(float(prog[k, q] - iop[k, q]) * 0.01, 1) for q in range(1, 9) if iop[k, q] > 0 and prog[k, q] > 0] for k in gi[::8]]
+        mt = tl[:, 26:36].astype(np.int64)
+        segc = np.diff(mt[:, ok], axis=1) / 4096.0
+        rec["clk_per_step_by_segment_every32"] = [[k] + [round(float(x), 1) for x in segc[k]] for k in range(0, len(segc), 32)]
+        rec["checkpoint_us"] = [[k] + [round(float(x - t0) * 0.01, 1) for x in prog[k, ok]] for k in range(0, len(seg), 64)]
     print(json.dumps(rec))
     b.close()
 
