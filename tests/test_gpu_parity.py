@@ -256,3 +256,23 @@ def test_chain_ring_laps_across_groups(eng, mode):
         oracle.fill_only(mode, texts[k], pats[k], S, 5, exp)
         assert int((b.directions(k) != exp).sum()) == 0, shapes[k]
     b.close()
+
+
+@pytest.mark.parametrize("gap", [0, 1, 5])
+def test_local_best_cell_near_last_column(eng, gap):
+    """Local strips with text profiles run no masked tail when g > 0 (sa_fill.hip process_strip): the
+    cells past column n are garbage whose H stays below the pair's best. Cases where the best cell is
+    in or next to the last column (the garbage right of it is as large as it gets), in every row
+    position of a strip and at body / chunk boundaries of n, with g = 0 (masked tail) beside them."""
+    S = synthetic.blast_matrix()
+    for k, (n, m) in enumerate([(1000, 1000), (1001, 999), (1024, 1088), (1040, 1023), (2063, 2050),
+                                (65, 130), (17, 127), (4097, 191)]):
+        t = synthetic.random_sequence(1500 + k, n, 4)
+        # the pattern ends with the text's last letters: the best local cell sits at column n
+        tail = t[-min(n, m):]
+        p = np.concatenate([synthetic.random_sequence(1600 + k, m - len(tail), 4), tail]).astype(np.int8)
+        for pp in (p, p[: m - 3]):
+            exp = oracle.align(1, t, pp, S, gap)
+            got = eng.align_pair(1, t, pp, S, gap, rows_per_lane=1)
+            got.pop("fill_us")
+            assert got == exp, (n, len(pp), gap)
