@@ -138,6 +138,9 @@ __device__ __forceinline__ bool keep_waiting(const FillArgs &a, uint64_t t0, int
 // inside one lap, so its tag is uniform.
 __device__ __forceinline__ int ring_slot(int c) { return (c + 63) & kRingMask; }
 __device__ __forceinline__ int ring_tag(int c) { return (int)((((uint32_t)(c + 63) >> 11) & 1u) ^ 1u) << 31; }
+// (c + 63) << 20: bit 31 is the complement of ring_tag(c); the asm bodies apply it with one v_bitop3
+// (tag = ~raw & 0x80000000), which saves the SALU masking per body
+__device__ __forceinline__ int ring_tag_raw(int c) { return (int)((uint32_t)(c + 63) << 20); }
 static_assert(kRing == 2048, "ring_tag assumes 2048-entry rings");
 constexpr int kConsEvery = 256;  // a consumer publishes its consumption word every this many columns
 
@@ -295,9 +298,10 @@ struct StepRegs {
     int T[4];    // text-profile words of the body (4 steps each)
     int g, kb;
     int pfaddr, pf;  // HP: LDS address of this lane's next feed slot, and the value read there
-    int pubaddr, pubtag;  // HN: this lane's publish address and the body's lap tag
-    int ctag;             // HP: lap tag the feed entries must carry
-    uint64_t bad;         // HP: lanes whose feed entry did not carry it
+    int pubaddr, pubtag;  // HN: this lane's publish address and the body's raw lap tag (ring_tag_raw)
+    int ctag;             // HP: raw lap tag the feed entries must carry
+    int msb;              // 0x80000000 in a VGPR (the bitop3 operand that applies raw tags)
+    uint64_t bad;         // HP: lanes 0..U-1 whose feed entry did not carry it
     template <int K>
     __device__ __forceinline__ void rotate()
     {
@@ -440,8 +444,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     bool pfTagged = false;  // pfVal already XORed with its tag by the asm body, bad lanes in pfBad
     uint64_t pfBad = 0;
     int consDone = 0;    // last consumption word written
-    // address of this lane's feed slot for the body starting at step base (column base+1+lane)
-    auto feed_addr = [&](int base) __attribute__((always_inline)) { return rin + ring_slot(base + 1 + lane); };
+    // address of this lane's feed slot for the body starting at step base (column base+1+lane): the
+    // body's 16 slots are one aligned run (ring_slot), so the wrap is applied to the uniform part only
+    // (lanes >= U read past it, into the next ring or the sink: their values are never used)
+    lds_int *rinLane = rin + lane;
+    const uint32_t rinLaneOff = lds_off(rinLane);
+    auto feed_addr = [&](int base) __attribute__((always_inline)) { return rinLane + ring_slot(base + 1); };
     auto prefetch = [&](int base) __attribute__((always_inline)) {
         if constexpr (HP)
         {
@@ -451,7 +459,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             pfVal = lds_ld(rin + ring_slot(c));
         }
     };
-    auto feed = [&](int base) __attribute__((always_inline)) {
+    // full: every lane 0..U-1 of this feed is needed and delivered (base + U <= n), so the check
+    // needs no per-body lane count
+    auto feed = [&](int base, bool full) __attribute__((always_inline)) {
         if constexpr (!HP)
         {
             // row 0 boundary. The zero is opaque on purpose: with a known-zero `old` the compiler
@@ -467,19 +477,23 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             const int tag = ring_tag(base + 1);
             // need = (1 << clamp(n - base, 0, U)) - 1, as four SALU ops (left to itself the compiler
             // clamps in VALU and round-trips through v_readfirstlane)
-            uint64_t need;
-            int cnt;
-            asm("s_sub_i32 %1, %2, %3\n\ts_max_i32 %1, %1, 0\n\ts_min_i32 %1, %1, %4\n\ts_bfm_b64 %0, %1, 0"
-                : "=s"(need), "=&s"(cnt)
-                : "s"(n), "s"(base), "i"(U)
-                : "scc");
+            uint64_t need = (1ull << U) - 1;
+            if (!full)  // (a constant at every call: the clamp is compiled out of the full bodies)
+            {
+                int cnt;
+                asm("s_sub_i32 %1, %2, %3\n\ts_max_i32 %1, %1, 0\n\ts_min_i32 %1, %1, %4\n\ts_bfm_b64 %0, %1, 0"
+                    : "=s"(need), "=&s"(cnt)
+                    : "s"(n), "s"(base), "i"(U)
+                    : "scc");
+            }
             int x = pfTagged ? pfVal : pfVal ^ tag;
-            const uint64_t bad = pfTagged ? pfBad : ballot(x < 0);
+            // (the asm bodies' mask already holds only lanes 0..U-1)
+            const uint64_t bad = pfTagged ? pfBad : (ballot(x < 0) & ((1ull << U) - 1));
             pfTagged = false;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_FEED_WAIT)
             if (base > 0 && false)  // timing ablation: never waits after the first feed (results wrong)
 #else
-            if (__builtin_expect((bad & need) != 0, 0))
+            if (__builtin_expect((full ? bad : (bad & need)) != 0, 0))
 #endif
             {
                 // a chained strip is paced by the strip above and often arrives a little early:
@@ -550,11 +564,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             lds_st(pubBase + (s0 & kRingMask), Q | ring_tag(s0 - 63));
         }
     };
+    int msbv;  // one VGPR for the strip (the compiler would rematerialize a literal per body)
+    asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     load_codes(0, TA);
     if constexpr (kAhead == 2) load_codes(U, TB);
     prefetch(0);
-    feed(0);
+    feed(0, false);
     const uint64_t tFed = a.timeline ? now_ticks() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
     uint64_t lbest = 0;
@@ -562,10 +578,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     // steady R = 1 bodies with int8 text profiles run hand-scheduled asm steps (sa_fill_steps.inc)
     constexpr bool kAsm = R == 1 && SK == kArr8 && SA_FILL_ASM;
     // pos: the body's place in its loop trip (0..3 in quads, 0..1 in pairs): odd bodies store the
-    // direction chunk (two bodies per chunk for R = 1), the trip's last one writes the consumption word
-    auto body = [&](auto kind, auto pos, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
+    // direction chunk (two bodies per chunk for R = 1), the trip's last one writes the consumption word.
+    // full: the next body's feed is known to be fully published (feed()) and s1 < nSteps.
+    auto body = [&](auto kind, auto pos, auto full, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
         constexpr int KIND = decltype(kind)::value;
         constexpr int POS = decltype(pos)::value;
+        constexpr bool FULL = decltype(full)::value;
         using second = std::integral_constant<bool, (POS & 1) == 1>;
         const int s1 = s0 + U;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
@@ -591,11 +609,15 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
             r.g = g;
             r.kb = kb;
-            r.pfaddr = HP ? (int)lds_off(feed_addr(s1)) : 0;
-            r.ctag = ring_tag(s1 + 1);
-            pub_wait(s0);  // the block ends with the publish write (HN)
+            r.pfaddr = HP ? (int)(rinLaneOff + 4u * (uint32_t)ring_slot(s1 + 1)) : 0;
+            r.ctag = ring_tag_raw(s1 + 1);
+            r.msb = msbv;
+            // the block ends with the publish write (HN); one backpressure check covers the bodies up
+            // to the trip's last (a quad from pos 0, a pair from pos 2)
+            if constexpr (POS == 0) pub_wait(s0 + 3 * U);
+            else if constexpr (POS == 2) pub_wait(s0 + U);
             r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
-            r.pubtag = ring_tag(s0 - 63);
+            r.pubtag = ring_tag_raw(s0 - 63);
             steps_asm<LOCAL, HN, HP>(r);  // with HP: reads the next body's feed after step 12
             if constexpr (HP)
             {
@@ -633,7 +655,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         if constexpr (LOCAL)
         {
             const int kmask = (1 << kb) - 1;
-            if (((s1 & kmask) == 0) || s1 >= nSteps)
+            if (((s1 & kmask) == 0) || (!FULL && s1 >= nSteps))
             {
                 const int blockBase = s0 & ~kmask;
                 sfor<R>([&](auto Rc) {
@@ -656,7 +678,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             }
         }
         if constexpr (!(kAsm && KIND == kSteady)) publish(s0);
-        feed(s1);
+        feed(s1, FULL);
         if constexpr (POS == (kAhead == 2 ? 3 : 1)) consumed(s1 + U);
     };
     using KSteady = std::integral_constant<int, kSteady>;
@@ -673,18 +695,18 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     {
         // bodies in quads up to `end` (a multiple of 2U), then at most one pair, after which the codes
         // loaded into TC / TD move back to TA / TB (once per phase)
-        auto phase = [&](auto kind, int end) __attribute__((always_inline)) {
+        auto phase = [&](auto kind, auto full, int end) __attribute__((always_inline)) {
             for (; s0 + 2 * U < end; s0 += 4 * U)
             {
-                body(kind, P0{}, s0, TA, TC);
-                body(kind, P1{}, s0 + U, TB, TD);
-                body(kind, P2{}, s0 + 2 * U, TC, TA);
-                body(kind, P3{}, s0 + 3 * U, TD, TB);
+                body(kind, P0{}, full, s0, TA, TC);
+                body(kind, P1{}, full, s0 + U, TB, TD);
+                body(kind, P2{}, full, s0 + 2 * U, TC, TA);
+                body(kind, P3{}, full, s0 + 3 * U, TD, TB);
             }
             if (s0 < end)
             {
-                body(kind, P2{}, s0, TA, TC);
-                body(kind, P3{}, s0 + U, TB, TD);
+                body(kind, P2{}, full, s0, TA, TC);
+                body(kind, P3{}, full, s0 + U, TB, TD);
                 s0 += 2 * U;
                 sfor<NT>([&](auto Qc) {
                     constexpr int q = decltype(Qc)::value;
@@ -693,27 +715,31 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 });
             }
         };
-        if constexpr (!kIsArr<SK>) phase(KStart{}, min(kWave, sTail));
-        phase(KSteady{}, sTail);
-        phase(KGeneric{}, nSteps);
+        // steady bodies whose next feed lies in columns 1..n (base + U <= n: every lane is needed and
+        // delivered, by a neighbour wave or by the I/O wave, which copies columns 1..n), then the rest
+        // of the steady bodies with a lane count
+        if constexpr (!kIsArr<SK>) phase(KStart{}, std::false_type{}, min(kWave, sTail));
+        phase(KSteady{}, std::true_type{}, min(sTail, max(0, (n - U) / (2 * U) * (2 * U))));
+        phase(KSteady{}, std::false_type{}, sTail);
+        phase(KGeneric{}, std::false_type{}, nSteps);
     }
     else
     {
         if constexpr (!kIsArr<SK>)
             for (; s0 < min(kWave, sTail); s0 += 2 * U)
             {
-                body(KStart{}, P0{}, s0, TA, TB);
-                body(KStart{}, P1{}, s0 + U, TB, TA);
+                body(KStart{}, P0{}, std::false_type{}, s0, TA, TB);
+                body(KStart{}, P1{}, std::false_type{}, s0 + U, TB, TA);
             }
         for (; s0 < sTail; s0 += 2 * U)
         {
-            body(KSteady{}, P0{}, s0, TA, TB);
-            body(KSteady{}, P1{}, s0 + U, TB, TA);
+            body(KSteady{}, P0{}, std::false_type{}, s0, TA, TB);
+            body(KSteady{}, P1{}, std::false_type{}, s0 + U, TB, TA);
         }
         for (; s0 < nSteps; s0 += 2 * U)
         {
-            body(KGeneric{}, P0{}, s0, TA, TB);
-            body(KGeneric{}, P1{}, s0 + U, TB, TA);
+            body(KGeneric{}, P0{}, std::false_type{}, s0, TA, TB);
+            body(KGeneric{}, P1{}, std::false_type{}, s0 + U, TB, TA);
         }
     }
     if (a.timeline && lane == 0)
@@ -949,7 +975,7 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
-__device__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
+__device__ __forceinline__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
     const int last = min(first + W, a.num_strips) - 1;

@@ -44,7 +44,9 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     D, M, T0, T1 = "%5", "%6", "%7", "%8"
     ACC0, ACC1 = "%9", "%10"
     # outputs first (Q .. acc1 = %0..%10, local extras %11..%15, then the feed value and its
-    # bad-lane mask), then inputs (T words, local g / kb, feed address and tag, publish address and tag)
+    # bad-lane mask), then inputs (T words, local g / kb, feed address and raw tag, publish address and
+    # raw tag, the sign-bit constant). A raw tag is (c + 63) << 20 of the slot's column c: its bit 31 is
+    # the lap parity, the complement of the tag (sa_fill.hip ring_tag); v_bitop3 applies it.
     h = 2 if hp else 0
     nout = (11 if not local else 16) + h
     PF = f"%{nout - 2}"
@@ -60,6 +62,9 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     if hp:
         k += 2
     PADDR, PTAG = f"%{k}", f"%{k + 1}"
+    if hn:
+        k += 2
+    MSB = f"%{k}"
     roles = [A, B, C]
     fregs = [FA, FB]
     out = []
@@ -103,15 +108,17 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
         roles = [b, c, a]
     if hp:
         out.append("s_waitcnt lgkmcnt(0)")  # the feed read (issued 4 steps ago) is there
-        # tag check: x = entry ^ expected tag (the value when it matches), bad lanes = x < 0; the
-        # publish below stands between the compare and the caller's SALU test of its mask
-        out.append(f"v_xor_b32_e32 {PF}, {CTAG}, {PF}")
+        # tag check: x = entry ^ expected tag (the value when it matches; bitop3 0xD2 = a ^ (~b & c)),
+        # bad lanes = x < 0 among the body's U feed lanes; the publish below stands between the
+        # compare and the caller's SALU test of the mask
+        out.append(f"v_bitop3_b32 {PF}, {PF}, {CTAG}, {MSB} bitop3:0xd2")
         out.append(f"v_cmp_gt_i32_e64 {BAD}, 0, {PF}")
+        out.append(f"s_and_b64 {BAD}, {BAD}, 0xffff")
     if hn:
         # publish: lanes 48..63 of the accumulated Q (now role B) with the body's lap tag; the write
         # stays in flight past the block (the compiler sees no LDS operation it would wait for)
         q_final = [A, B, C][U % 3]
-        out.append(f"v_or_b32_e32 {T0}, {PTAG}, {q_final}")
+        out.append(f"v_bitop3_b32 {T0}, {q_final}, {PTAG}, {MSB} bitop3:0xf2")  # a | (~b & c)
         out.append(f"ds_write_b32 {PADDR}, {T0}")
     return "\\n\\t".join(out)
 
@@ -144,7 +151,9 @@ def main():
                 if local:
                     lines.append("          , \"+v\"(r.acc2), \"+v\"(r.bm), \"=&v\"(X), \"=&v\"(t2), \"=&v\"(key)")
                 if hp:
-                    lines.append("          , \"=&v\"(r.pf), \"=s\"(r.bad)")
+                    # early-clobber: the mask is written before the publish reads its raw tag (an SGPR
+                    # input the compiler could otherwise assign to the same register)
+                    lines.append("          , \"=&v\"(r.pf), \"=&s\"(r.bad)")
                 ins = "\"v\"(r.T[0]), \"v\"(r.T[1]), \"v\"(r.T[2]), \"v\"(r.T[3])"
                 if local:
                     ins += ", \"s\"(r.g), \"s\"(r.kb)"
@@ -152,7 +161,9 @@ def main():
                     ins += ", \"v\"(r.pfaddr), \"s\"(r.ctag)"
                 if hn:
                     ins += ", \"v\"(r.pubaddr), \"s\"(r.pubtag)"
-                lines.append(f"        : {ins});")
+                if hn or hp:
+                    ins += ", \"v\"(r.msb)"
+                lines.append(f"        : {ins}" + (" : \"scc\");" if hp else ");"))
                 lines.append("    (void)D; (void)M; (void)t0; (void)t1; (void)X; (void)t2; (void)key;")
                 lines.append(f"    r.rotate<{rot(U)}>();")
                 lines.append("}")
