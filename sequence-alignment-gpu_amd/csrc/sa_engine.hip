@@ -844,7 +844,11 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     x.results = pl->d_results;
     x.A = pl->A;
     std::memcpy(x.alphabet, pl->alphabet, 33);
-    launch_expand(x, np, st);
+    // records per pair: one per row (row walk, R = 1) or per column (column walk)
+    int64_t maxRecs = 1;
+    for (const PairDesc &d : pl->pairs)
+        maxRecs = std::max<int64_t>(maxRecs, (int64_t)(pl->R == 1 ? d.pattern_len : d.text_len));
+    launch_expand(x, np, maxRecs, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "expand_kernel")) return rc;
     if (tmPath)

@@ -52,12 +52,16 @@ struct ExpandArgs {
     char *out_text, *out_pattern;
     sa_result *results;
     int32_t A;
+    int32_t chunk_recs;  // records per expansion block (launch_expand sets it)
     char alphabet[33];
 };
 
 // one wave per pair: row walk (R = 1) or column walk (R >= 2)
 void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st);
-// every plan: records -> aligned strings and sa_result
-void launch_expand(const ExpandArgs &a, int np, hipStream_t st);
+// every plan: records -> aligned strings and sa_result; max_records bounds h.nrec over the pairs
+// (pattern rows for the row walk, text columns for the column walk)
+constexpr int kChunkRecs = 2048;  // records per expansion block (at least)
+constexpr int kMaxChunks = 64;    // blocks per pair (chunks past a pair's records exit at once)
+void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st);
 
 }  // namespace sa

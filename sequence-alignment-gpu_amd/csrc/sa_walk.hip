@@ -34,6 +34,7 @@
 // partial batches and restages run the same logic as a C++ loop.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 
@@ -595,7 +596,34 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 // ------------------------------------------------------------------------------------------------
 // expansion: records -> aligned strings (forward order) and the per-pair result
 // ------------------------------------------------------------------------------------------------
+// Grid (chunks, pairs): block c of a pair expands records [c * kChunkRecs, (c+1) * kChunkRecs), so a
+// single long pair spreads over up to kMaxChunks CUs (one workgroup took 0.18 ms at 32768^2). Each
+// block first sums every record of the pair (the total length L fixes the forward positions) and
+// those before its chunk (its starting position and letter counts) in one strided pass — O(N) reads
+// per block, served by L2 — then scans its own records. Block 0 also writes the trailing run and
+// the sa_result.
 constexpr int kExpThreads = 256;
+
+// block-wide sums of two 64-bit values (tree in LDS)
+__device__ __forceinline__ void block_sum2(int64_t &x, int64_t &y, int64_t *lds)
+{
+    const int t = threadIdx.x;
+    lds[t] = x;
+    lds[kExpThreads + t] = y;
+    __syncthreads();
+    for (int d = kExpThreads / 2; d > 0; d >>= 1)
+    {
+        if (t < d)
+        {
+            lds[t] += lds[t + d];
+            lds[kExpThreads + t] += lds[kExpThreads + t + d];
+        }
+        __syncthreads();
+    }
+    x = lds[0];
+    y = lds[kExpThreads];
+    __syncthreads();
+}
 
 __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *lds, int64_t &total)
 {
@@ -615,35 +643,45 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *lds,
     return incl - v;
 }
 
+// ops and letters consumed along the free coordinate by record v, packed (each < 2^31 per pair)
+__device__ __forceinline__ int64_t rec_counts(int v) { return ((int64_t)((v >> 1) + 1) << 32) | (int64_t)((v >> 1) + (v & 1)); }
+
 __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
 {
-    __shared__ int64_t scan[kExpThreads];
+    __shared__ int64_t scan[2 * kExpThreads];
     __shared__ char alpha[40];
-    const int p = blockIdx.x;
+    const int p = blockIdx.y;
     const int t = threadIdx.x;
-    if (t < 33) alpha[t] = a.alphabet[t];
     const TbHead h = a.heads[p];
+    const int N = h.nrec;
+    const int c0 = (int)blockIdx.x * a.chunk_recs;
+    if (blockIdx.x > 0 && c0 >= N) return;  // (uniform per block)
+    if (t < 33) alpha[t] = a.alphabet[t];
     const PairDesc pd = a.pairs[p];
     const int32_t *rec = a.rec + pd.rec_off;
     const int8_t *tx = a.text + pd.text_off;
     const int8_t *px = a.pattern + pd.pattern_off;
     char *ot = a.out_text + pd.out_off;
     char *op = a.out_pattern + pd.out_off;
-    const int N = h.nrec;
-    const int per = (N + kExpThreads - 1) / kExpThreads;
-    const int lo = min(N, t * per), hi = min(N, lo + per);
-    // pass 1: ops and letters consumed along the walk's free coordinate, this thread's records
-    int64_t cnt = 0, cons = 0;
-    for (int q = lo; q < hi; ++q)
+    const int cend = min(N, c0 + a.chunk_recs);
+    // pass 0: totals over the pair and the prefix before this chunk
+    int64_t tot = 0, pre = 0;
+    for (int q = t; q < N; q += kExpThreads)
     {
-        const int v = rec[q];
-        cnt += (v >> 1) + 1;
-        cons += (v >> 1) + (v & 1);
+        const int64_t x = rec_counts(rec[q]);
+        tot += x;
+        pre += q < c0 ? x : 0;
     }
-    int64_t tot;  // both sums in one 64-bit scan (each < 2^31)
-    const int64_t ex = block_exclusive_scan((cnt << 32) | cons, scan, tot);
-    const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
+    block_sum2(tot, pre, scan);
     const int64_t totCnt = tot >> 32, totCons = tot & 0xffffffffll;
+    // pass 1: this thread's records of the chunk
+    const int per = (cend - c0 + kExpThreads - 1) / kExpThreads;
+    const int lo = min(cend, c0 + t * per), hi = min(cend, lo + per);
+    int64_t mine = 0;
+    for (int q = lo; q < hi; ++q) mine += rec_counts(rec[q]);
+    int64_t chunkTot;
+    const int64_t ex = block_exclusive_scan(mine, scan, chunkTot) + pre;
+    const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
     const int64_t L = totCnt + h.tail;
     const char GAP = alpha[a.A];
     // pass 2
@@ -692,6 +730,7 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
             j -= 1;
         }
     }
+    if (blockIdx.x != 0) return;
     // the trailing run: forward positions 0 .. tail-1, ending at the walk's last cell
     {
         const int64_t iT = h.kind == kRecRows ? (int64_t)h.i0 - N : (int64_t)h.i0 - totCons;
@@ -745,9 +784,14 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
     else launch_walk_m<false>(R, a, np, st);
 }
 
-void launch_expand(const ExpandArgs &a, int np, hipStream_t st)
+void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st)
 {
-    hipLaunchKernelGGL(expand_kernel, dim3(np), dim3(kExpThreads), 0, st, a);
+    ExpandArgs x = a;
+    const int64_t recs = std::max<int64_t>(1, max_records);
+    const int64_t per = std::max<int64_t>(kChunkRecs, (recs + kMaxChunks - 1) / kMaxChunks);
+    x.chunk_recs = (int)per;
+    const int chunks = (int)((recs + per - 1) / per);
+    hipLaunchKernelGGL(expand_kernel, dim3(chunks, np), dim3(kExpThreads), 0, st, x);
 }
 
 }  // namespace sa

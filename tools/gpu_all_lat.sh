@@ -1,0 +1,6 @@
+#!/bin/bash
+# full GPU test suite, then the end-to-end latency trace
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
+bash tools/prof_latency.sh
