@@ -77,21 +77,52 @@ __global__ void encode_text_kernel(const int8_t *text, const int8_t *pattern, co
         }
         return;
     }
-    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < pd.text_len;
-         x += (uint64_t)gridDim.x * blockDim.x)
+    // every position of the code block, padding included (zero scores / letter 0): the block is not
+    // cleared beforehand
+    const int64_t n = (int64_t)pd.text_len;
+    auto letter = [&](int64_t x) { return min(max((int)text[pd.text_off + x], 0), A - 1); };
+    if (SK == kArr8)
     {
-        int c = text[pd.text_off + x];
-        c = min(max(c, 0), A - 1);
-        if (SK == kArr8)
+        // copy sh of row r holds S[r][t[p - kPad - sh]] at byte p. One item = (dword w, row r): the
+        // four copies' dwords at bytes 4w .. 4w+3, from the 7 letters x0-3 .. x0+3 (x0 = 4w - kPad)
+        // and the score table staged in LDS
+        __shared__ int8_t tab[32 * 32];
+        for (int e = threadIdx.x; e < A * A; e += blockDim.x) tab[e] = (int8_t)table[e];
+        __syncthreads();
+        uint32_t *w32 = reinterpret_cast<uint32_t *>(codes + pd.code_off);
+        const uint64_t rowW = pd.code_len / 4;  // dwords per row (code_len is a multiple of 4)
+        const uint64_t items = rowW * (uint64_t)A;
+        for (uint64_t it = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; it < items; it += (uint64_t)gridDim.x * blockDim.x)
         {
-            int8_t *b8 = reinterpret_cast<int8_t *>(codes + pd.code_off);
-            for (int r = 0; r < A; ++r)
-                for (int sh = 0; sh < 4; ++sh) b8[((uint64_t)r * 4 + sh) * pd.code_len + kPad + x + sh] = (int8_t)table[r * A + c];
+            const uint64_t w = it % rowW;
+            const int r = (int)(it / rowW);
+            const int64_t x0 = 4 * (int64_t)w - kPad;
+            uint32_t sc[7];  // score byte of each letter (0 outside the text)
+            for (int k = 0; k < 7; ++k)
+            {
+                const int64_t x = x0 - 3 + k;
+                sc[k] = (x >= 0 && x < n) ? (uint32_t)(uint8_t)tab[r * A + letter(x)] : 0u;
+            }
+            for (int sh = 0; sh < 4; ++sh)
+                w32[((uint64_t)r * 4 + sh) * rowW + w] =
+                    sc[3 - sh] | (sc[4 - sh] << 8) | (sc[5 - sh] << 16) | (sc[6 - sh] << 24);
         }
-        else if (SK == kArr)
-            for (int r = 0; r < A; ++r) codes[pd.code_off + (uint64_t)r * pd.code_len + kPad + x] = table[r * A + c];
+        return;
+    }
+    for (uint64_t pp = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; pp < pd.code_len;
+         pp += (uint64_t)gridDim.x * blockDim.x)
+    {
+        const int64_t x = (int64_t)pp - kPad;
+        if (SK == kArr)
+        {
+            const int c = (x >= 0 && x < n) ? letter(x) : -1;
+            for (int r = 0; r < A; ++r) codes[pd.code_off + (uint64_t)r * pd.code_len + pp] = c >= 0 ? table[r * A + c] : 0;
+        }
         else
-            codes[pd.code_off + kPad + x] = SK == kProf ? 8 * c : c;
+        {
+            const int c = (x >= 0 && x < n) ? letter(x) : 0;
+            codes[pd.code_off + pp] = SK == kProf ? 8 * c : c;
+        }
     }
 }
 // ------------------------------------------------------------------------------------------------
@@ -244,6 +275,7 @@ struct sa_plan {
     std::vector<StripDesc> strips;
     char alphabet[33] = {0};
     uint32_t epoch = 0;
+    uint32_t *epoch_src = nullptr;  // workspace plans draw epochs from their DeviceCtx (see there)
     hipStream_t own = nullptr;
     // device
     PairDesc *d_pairs = nullptr;
@@ -262,6 +294,12 @@ struct sa_plan {
     uint64_t bytes_total = 0, bytes_masks = 0, out_bytes = 0;
     bool filled = false;
     bool borrowed = false;  // device buffers and stream belong to a DeviceCtx workspace (sa_align_pair)
+    // workspace plans: the uploaded region [pairs .. inputs .. ctrl] and the downloaded region
+    // [ctrl | results | out_text | out_pattern] are contiguous in the arena (one copy each way)
+    char *d_up = nullptr, *d_dn = nullptr;
+    size_t up_bytes = 0, dn_bytes = 0;
+    int8_t *d_ws_text = nullptr, *d_ws_pattern = nullptr;
+    bool ctrl_ready = false;  // the control word was uploaded zeroed (no memset before the next fill)
     std::vector<int32_t> h_prof, h_table;  // host copies the (asynchronous) uploads read from
 };
 
@@ -368,6 +406,17 @@ struct DeviceCtx {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     char *arena = nullptr;
     size_t arena_bytes = 0;
+    // pinned host staging: a call's uploads leave in one DMA copy and its results come back in one
+    // (pageable copies go through the runtime's staging blits, ~20 us each)
+    char *pinned = nullptr;
+    size_t pinned_bytes = 0;
+    // granules live in a buffer of their own (zeroed when allocated, never used for anything else)
+    // and carry epochs that only grow across calls: a granule left by an earlier call never
+    // matches, so the area needs no clearing per call. (Inside the shared arena it would: stale
+    // records or scores there can look like a granule of the current epoch.)
+    char *bnd = nullptr;
+    size_t bnd_bytes = 0;
+    uint32_t epoch = 0;
 };
 
 std::mutex g_ctx_mu;
@@ -380,6 +429,12 @@ void release_ctx(DeviceCtx *c)
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(c->device);
     if (c->arena) (void)hipFree(c->arena);
+    if (c->pinned) (void)hipHostFree(c->pinned);
+    if (c->bnd) (void)hipFree(c->bnd);
+    c->bnd = nullptr;
+    c->bnd_bytes = 0;
+    c->pinned = nullptr;
+    c->pinned_bytes = 0;
     if (c->e0) (void)hipEventDestroy(c->e0);
     if (c->e1) (void)hipEventDestroy(c->e1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -448,11 +503,56 @@ int ctx_prepare(DeviceCtx *c, size_t bytes)
     return SA_OK;
 }
 
+// Makes sure c has a granule buffer of at least `bytes` (zeroed when (re)allocated).
+int ctx_bnd(DeviceCtx *c, size_t bytes)
+{
+    if (c->bnd_bytes >= bytes) return SA_OK;
+    if (c->bnd)
+    {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)hipFree(c->bnd);
+        c->bnd = nullptr;
+        c->bnd_bytes = 0;
+    }
+    const size_t want = std::max(bytes, (size_t)1 << 16);
+    if (hipMalloc((void **)&c->bnd, want) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        c->bnd = nullptr;
+        return fail(SA_ERR_NOMEM, "device allocation of " + std::to_string(want) + " bytes failed");
+    }
+    c->bnd_bytes = want;
+    HIP_TRY(hipMemsetAsync(c->bnd, 0, want, c->stream));
+    return SA_OK;
+}
+
+// Makes sure c has a pinned staging buffer of at least `bytes`.
+int ctx_pinned(DeviceCtx *c, size_t bytes)
+{
+    if (c->pinned_bytes >= bytes) return SA_OK;
+    if (c->pinned)
+    {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        (void)hipHostFree(c->pinned);
+        c->pinned = nullptr;
+        c->pinned_bytes = 0;
+    }
+    const size_t want = std::max(bytes, (size_t)1 << 20);
+    HIP_TRY(hipHostMalloc((void **)&c->pinned, want, hipHostMallocDefault));
+    c->pinned_bytes = want;
+    return SA_OK;
+}
+
 constexpr size_t kArenaAlign = 256;
 size_t arena_round(size_t b) { return (std::max<size_t>(b, 16) + kArenaAlign - 1) / kArenaAlign * kArenaAlign; }
 
-int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, DeviceCtx *ws, size_t ws_extra,
-                sa_plan **out);
+// host inputs a workspace plan uploads together with its descriptors (sa_align_pair)
+struct OneShotInputs {
+    const char *text = nullptr, *pattern = nullptr;
+    uint64_t n = 0, m = 0;
+};
+int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, DeviceCtx *ws,
+                const OneShotInputs *in, sa_plan **out);
 
 }  // namespace
 
@@ -469,7 +569,7 @@ int sa_device_count(int *count)
 
 int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, sa_plan **out)
 {
-    return plan_create(P, pairs, np, device, nullptr, 0, out);
+    return plan_create(P, pairs, np, device, nullptr, nullptr, out);
 }
 
 }  // extern "C"
@@ -477,10 +577,11 @@ int sa_plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int dev
 namespace {
 
 // Builds a plan. With `ws` (a locked DeviceCtx, current device set) every device buffer is carved
-// from the context's arena (grown to hold them plus `ws_extra` bytes at its end for the caller)
-// and the uploads are asynchronous on the context's stream; otherwise buffers are hipMalloc'd.
-int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, DeviceCtx *ws, size_t ws_extra,
-                sa_plan **out)
+// from the context's arena, the host inputs `in` too, and everything the fill reads from the host
+// goes up in one asynchronous copy from the context's pinned buffer; otherwise buffers are
+// hipMalloc'd and uploaded one by one.
+int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device, DeviceCtx *ws,
+                const OneShotInputs *in, sa_plan **out)
 {
     if (!P || !out || np < 0 || (np > 0 && !pairs) || !P->score_matrix)
         return fail(SA_ERR_INVALID, "sa_plan_create: null argument");
@@ -637,58 +738,93 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
     const size_t nstr = std::max<size_t>(1, pl->strips.size()), npp = std::max<size_t>(1, np);
     const size_t codeB = 4 * code_bytes + 16, bndB = granules * 8 + 16, bestB = sizeof(uint64_t) * nstr;
     struct Buf { void **ptr; size_t bytes; };
+    const uint64_t inN = in ? in->n : 0, inM = in ? in->m : 0;
+    // order matters for workspace plans: [pairs .. ctrl] is the upload region, [ctrl .. out_pattern]
+    // the download region (zero-sized entries are skipped)
     const Buf bufs[] = {
         {(void **)&pl->d_pairs, sizeof(PairDesc) * npp},
         {(void **)&pl->d_strips, sizeof(StripDesc) * nstr},
         {(void **)&pl->d_prof, sizeof(int32_t) * 4},
         {(void **)&pl->d_table, sizeof(int32_t) * A * A},
+        {(void **)&pl->d_ws_text, in ? inN + 16 : 0},
+        {(void **)&pl->d_ws_pattern, in ? inM + 16 : 0},
+        {(void **)&pl->d_ctrl, sizeof(Control)},
+        {(void **)&pl->d_results, sizeof(sa_result) * npp},
+        {(void **)&pl->d_out_text, outb + 16},
+        {(void **)&pl->d_out_pattern, outb + 16},
         {(void **)&pl->d_codes, codeB},
         // (+8 KiB: the traceback's plane prefetch may read a few chunks past a strip)
         {(void **)&pl->d_masks, pl->bytes_masks + 8192},
-        {(void **)&pl->d_bnd, bndB},
+        {(void **)&pl->d_bnd, ws ? 0 : bndB},  // (workspace plans: the context's granule buffer)
         {(void **)&pl->d_best, bestB},
         {(void **)&pl->d_score, sizeof(int32_t) * npp},
-        {(void **)&pl->d_ctrl, sizeof(Control)},
         {(void **)&pl->d_rec, 4 * recw + 16},
         {(void **)&pl->d_heads, sizeof(TbHead) * npp},
-        {(void **)&pl->d_out_text, outb + 16},
-        {(void **)&pl->d_out_pattern, outb + 16},
-        {(void **)&pl->d_results, sizeof(sa_result) * npp},
     };
     int rc = SA_OK;
     if (ws)
     {
         size_t total = 0;
-        for (const Buf &b : bufs) total += arena_round(b.bytes);
-        if ((rc = ctx_prepare(ws, total + ws_extra)) != SA_OK) { delete pl; restore(); return rc; }
+        for (const Buf &b : bufs) total += b.bytes ? arena_round(b.bytes) : 0;
+        if ((rc = ctx_prepare(ws, total)) != SA_OK) { delete pl; restore(); return rc; }
         size_t off = 0;
         for (const Buf &b : bufs)
         {
+            if (!b.bytes) continue;
             *b.ptr = ws->arena + off;
             off += arena_round(b.bytes);
         }
-        pl->bytes_total = total;
+        if ((rc = ctx_bnd(ws, bndB)) != SA_OK) { delete pl; restore(); return rc; }
+        pl->d_bnd = (uint64_t *)ws->bnd;
+        pl->bytes_total = total + bndB;
         pl->borrowed = true;
         pl->own = ws->stream;
+        pl->epoch_src = &ws->epoch;
+        pl->d_up = (char *)pl->d_pairs;
+        pl->up_bytes = (size_t)((char *)pl->d_ctrl - pl->d_up) + sizeof(Control);
+        pl->d_dn = (char *)pl->d_ctrl;
+        pl->dn_bytes = (size_t)(pl->d_out_pattern - pl->d_dn) + outb + 16;
+        if ((rc = ctx_pinned(ws, std::max(pl->up_bytes, pl->dn_bytes))) != SA_OK) { delete pl; restore(); return rc; }
+        // one upload: descriptors, tables, the inputs and a zeroed control word at their arena
+        // offsets. The code block is written whole by the encode kernel, granules carry growing
+        // epochs in their own buffer (DeviceCtx) and every strip writes its best key, so nothing
+        // else needs clearing.
+        char *h = ws->pinned;
+        auto put = [&](const void *dptr, const void *src, size_t bytes) {
+            if (bytes) std::memcpy(h + ((const char *)dptr - pl->d_up), src, bytes);
+        };
+        put(pl->d_pairs, pl->pairs.data(), sizeof(PairDesc) * np);
+        put(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size());
+        put(pl->d_prof, prof.data(), sizeof(int32_t) * 4);
+        put(pl->d_table, table.data(), sizeof(int32_t) * A * A);
+        put(pl->d_ws_text, in->text, inN);
+        put(pl->d_ws_pattern, in->pattern, inM);
+        std::memset(h + ((char *)pl->d_ctrl - pl->d_up), 0, sizeof(Control));
+        if (hipMemcpyAsync(pl->d_up, h, pl->up_bytes, hipMemcpyHostToDevice, pl->own) != hipSuccess)
+        {
+            free_plan(pl);
+            restore();
+            return fail(SA_ERR_HIP, "plan upload failed");
+        }
+        pl->ctrl_ready = true;
+        restore();
+        *out = pl;
+        return SA_OK;
     }
-    else
-    {
-        for (const Buf &b : bufs)
-            if (rc == SA_OK) { rc = dmalloc(b.ptr, b.bytes); pl->bytes_total += b.bytes; }
-        if (rc != SA_OK) { free_plan(pl); restore(); return rc; }
-        if (hipStreamCreateWithFlags(&pl->own, hipStreamNonBlocking) != hipSuccess) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "stream creation failed"); }
-    }
+    for (const Buf &b : bufs)
+        if (rc == SA_OK && b.bytes) { rc = dmalloc(b.ptr, b.bytes); pl->bytes_total += b.bytes; }
+    if (rc != SA_OK) { free_plan(pl); restore(); return rc; }
+    if (hipStreamCreateWithFlags(&pl->own, hipStreamNonBlocking) != hipSuccess) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "stream creation failed"); }
     // uploads (asynchronous on the plan's stream; the host sources live in the plan)
     hipStream_t st = pl->own;
     bool okc = hipMemcpyAsync(pl->d_pairs, pl->pairs.data(), sizeof(PairDesc) * np, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemcpyAsync(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemcpyAsync(pl->d_prof, prof.data(), sizeof(int32_t) * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemcpyAsync(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice, st) == hipSuccess &&
-               hipMemsetAsync(pl->d_codes, 0, codeB, st) == hipSuccess &&
                hipMemsetAsync(pl->d_bnd, 0, bndB, st) == hipSuccess &&
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
     // a plan of its own is complete when sa_plan_create returns (callers fill on other streams)
-    if (okc && !ws) okc = hipStreamSynchronize(st) == hipSuccess;
+    if (okc) okc = hipStreamSynchronize(st) == hipSuccess;
     if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
     restore();
     *out = pl;
@@ -713,15 +849,19 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
     if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
     pl->d_text_in = (const int8_t *)d_text;
     pl->d_pattern_in = (const int8_t *)d_pattern;
-    pl->epoch += 1;
-    if (pl->epoch == 0) pl->epoch = 1;
-    HIP_TRY(hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st));
+    uint32_t *es = pl->epoch_src ? pl->epoch_src : &pl->epoch;
+    if (++*es == 0) ++*es;
+    pl->epoch = *es;
+    if (!pl->ctrl_ready) HIP_TRY(hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st));
+    pl->ctrl_ready = false;
     const int np = (int)pl->pairs.size();
     if (np > 0)
     {
         uint64_t nmax = 1;
         for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, std::max(d.text_len, d.pattern_len));
-        const int gx = (int)std::min<uint64_t>((nmax + 255) / 256, 64);
+        // (text profiles: one thread per dword and alphabet row)
+        const uint64_t work = pl->sk == kArr8 ? (nmax / 4 + kPad) * (uint64_t)pl->A : nmax;
+        const int gx = (int)std::min<uint64_t>((work + 255) / 256, 1024);
         for (int y0 = 0; y0 < np; y0 += 65534)
         {
             // pairs beyond 65535 are handled by re-basing the pair pointer
@@ -981,49 +1121,48 @@ int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *
     if (!P || !out || (n && !text) || (m && !pattern)) return fail(SA_ERR_INVALID, "sa_align_pair: null argument");
     const bool fillOnly = !at && !ap;  // -DBENCHMARK contract: DP fill only
     if (!fillOnly && cap < n + m) return fail(SA_ERR_INVALID, "sa_align_pair: output capacity below text_len + pattern_len");
-    for (uint64_t x = 0; x < n; ++x)
-        if (text[x] < 0 || text[x] >= P->alphabet_size) return fail(SA_ERR_INVALID, "text byte outside the alphabet");
-    for (uint64_t x = 0; x < m; ++x)
-        if (pattern[x] < 0 || pattern[x] >= P->alphabet_size) return fail(SA_ERR_INVALID, "pattern byte outside the alphabet");
+    // (letters outside the alphabet are reported by the encode kernel: SA_ERR_INVALID below)
     DeviceCtx *ws = device_ctx(device);
     if (!ws) return fail(SA_ERR_INVALID, "sa_align_pair: bad device");
     std::lock_guard<std::mutex> lk(ws->mu);
     DeviceGuard dg(device);
     if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
-    // the plan and both inputs live in the device's cached arena (inputs at its end)
-    const size_t inB = arena_round(n + 16) + arena_round(m + 16);
+    // the plan, its uploads and both inputs live in the device's cached arena: one copy up (plan
+    // creation), one copy down (control word, result, strings) and the kernels in between
     sa_pair pr{0, n, 0, m};
+    OneShotInputs in;
+    in.text = text;
+    in.n = n;
+    in.pattern = pattern;
+    in.m = m;
     sa_plan *pl = nullptr;
-    int rc = plan_create(P, &pr, 1, device, ws, inB, &pl);
+    int rc = plan_create(P, &pr, 1, device, ws, &in, &pl);
     if (rc) return rc;
     std::unique_ptr<sa_plan, void (*)(sa_plan *)> hold(pl, free_plan);
     HIP_TRY(hipSetDevice(device));
     hipStream_t st = ws->stream;
-    int8_t *dt = (int8_t *)ws->arena + pl->bytes_total, *dp = dt + arena_round(n + 16);
-    if (n) HIP_TRY(hipMemcpyAsync(dt, text, n, hipMemcpyHostToDevice, st));
-    if (m) HIP_TRY(hipMemcpyAsync(dp, pattern, m, hipMemcpyHostToDevice, st));
     HIP_TRY(hipEventRecord(ws->e0, st));
-    if ((rc = sa_plan_fill(pl, dt, dp, st))) return rc;
+    if ((rc = sa_plan_fill(pl, pl->d_ws_text, pl->d_ws_pattern, st))) return rc;
     HIP_TRY(hipEventRecord(ws->e1, st));
-    Control ctrl;
-    if (!fillOnly)
-    {
-        if ((rc = sa_plan_traceback(pl, st))) return rc;
-        // everything comes back in one synchronisation: the result, the abort word and the
-        // n + m bytes of output capacity (the strings are the first num_alignment_bytes of them)
-        HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result), hipMemcpyDeviceToHost, st));
-        if (n + m)
-        {
-            const uint64_t off = pl->pairs[0].out_off;
-            if (at) HIP_TRY(hipMemcpyAsync(at, pl->d_out_text + off, n + m, hipMemcpyDeviceToHost, st));
-            if (ap) HIP_TRY(hipMemcpyAsync(ap, pl->d_out_pattern + off, n + m, hipMemcpyDeviceToHost, st));
-        }
-    }
-    HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
+    if (!fillOnly && (rc = sa_plan_traceback(pl, st))) return rc;
+    // [ctrl | result | out_text | out_pattern]; fill-only needs the control word alone
+    const size_t dn = fillOnly ? sizeof(Control) : pl->dn_bytes;
+    HIP_TRY(hipMemcpyAsync(ws->pinned, pl->d_dn, dn, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    const char *h = ws->pinned;
+    Control ctrl;
+    std::memcpy(&ctrl, h, sizeof(Control));
     // also in fill-only mode: a fill whose hand-off timed out produced garbage, not a fill time
     if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
+    if (!fillOnly)
+    {
+        std::memcpy(out, h + ((char *)pl->d_results - pl->d_dn), sizeof(sa_result));
+        const uint64_t L = std::min<uint64_t>(out->num_alignment_bytes, n + m);
+        const uint64_t off = pl->pairs[0].out_off;
+        if (at && L) std::memcpy(at, h + ((char *)pl->d_out_text - pl->d_dn) + off, L);
+        if (ap && L) std::memcpy(ap, h + ((char *)pl->d_out_pattern - pl->d_dn) + off, L);
+    }
     if (fill_us)
     {
         float ms = 0.f;
