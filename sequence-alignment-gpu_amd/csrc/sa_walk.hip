@@ -18,8 +18,10 @@
 // p. Lane l of the windows is the l-th line of the current batch of 64 lines, walked from lane 63
 // down; window w covers the 16 positions after window w-1 along the free coordinate. When W0 holds
 // nothing at or after u the windows rotate (W0 <- W1 ...); after eight the kernel restages. Local
-// mode also reads STOP windows (odd bit = STOP) and ends the walk at a STOP cell. The borders are
-// encoded in the windows (global: column 0 TOP / row 0 LEFT; local: STOP), so they need no tests.
+// mode marks a STOP cell by setting both of its bits: the search then finds its even bit, and bit
+// p ^ 1 (set only for STOP: an even find is otherwise a run end without DIAG, an odd find has its
+// even bit clear) ends the walk. The borders are encoded in the windows (global: column 0 TOP /
+// row 0 LEFT; local: STOP), so they need no tests.
 //
 // ROW WALK (R = 1): lanes = the 64 rows of a strip (lane k = row k), windows = 8 x 16 columns left of
 //   the strip's entry column, built from the lane's own plane words (sa_layout.h: R = 1 slot e =
@@ -82,7 +84,7 @@ __device__ __forceinline__ uint32_t window(uint32_t E, uint32_t D) { return spre
 // every lane's chunks, else from global memory (uniform decision). sb = the strip's first dword.
 template <bool LOCAL>
 __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const uint32_t *pf, int pfclo, int jo,
-                                         int lane, uint32_t (&W)[8], uint32_t (&S)[8])
+                                         int lane, uint32_t (&W)[8])
 {
     const int etop = jo - 1 + lane;   // slot of column jo in this lane's stream (R = 1: e = j - 1 + k)
     const int c0 = etop >> 5;         // (arithmetic shift: etop >= -1)
@@ -117,7 +119,7 @@ __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const 
         const int z = jo - 32 * s;  // column of bit 0 (uniform): bits t < z are columns >= 1
         const uint32_t vm = z >= 32 ? ~0u : (z <= 0 ? 0u : ((1u << z) - 1u));
         const uint32_t c0b = (z >= 0 && z < 32) ? (1u << z) : 0u;  // column 0
-        uint32_t T, D, St = 0;
+        uint32_t T, D;
         if constexpr (!LOCAL)
         {
             D = X & vm;                     // plane 0 = DIAG
@@ -125,17 +127,13 @@ __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const 
         }
         else
         {
-            D = (X & vm) | c0b;             // DIAG or STOP; column 0: STOP (the border ends the walk)
-            T = Y & ~X & vm;
-            St = (X & Y & vm) | c0b;
+            // plane 0 = DIAG or STOP, plane 1 = TOP or STOP: STOP (both) sets both bits, and so does
+            // column 0 (the border ends the walk)
+            D = (X & vm) | c0b;
+            T = (Y & vm) | c0b;
         }
         W[2 * s] = window(T, D);
         W[2 * s + 1] = window(T >> 16, D >> 16);
-        if constexpr (LOCAL)
-        {
-            S[2 * s] = spread16(St) << 1;
-            S[2 * s + 1] = spread16(St >> 16) << 1;
-        }
     });
 }
 
@@ -144,7 +142,7 @@ __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const 
 // is the row-0 border. mb = the pair's first strip's first dword.
 template <int R, bool LOCAL>
 __device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_t sstride, int J0, int G0, int lane,
-                                         uint32_t (&W)[8], uint32_t (&S)[8])
+                                         uint32_t (&W)[8])
 {
     using G_ = Geo<R>;
     const int j = J0 - 63 + lane;
@@ -179,7 +177,7 @@ __device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_
         constexpr int w = decltype(Wc)::value;
         const int G = G0 - w;
         const uint32_t x0 = f0[w], x1 = f1[w];
-        uint32_t E, D, St = 0;
+        uint32_t E, D;
         if constexpr (!LOCAL)
         {
             D = x0;                                   // DIAG
@@ -189,13 +187,11 @@ __device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_
         else
         {
             D = x0;                                   // DIAG or STOP
-            E = ~x0 & ~x1 & 0xffffu;                  // LEFT
-            St = x0 & x1;
-            if (G == -1) { D = 1; E = 0; St = 1; }    // row 0: the border ends the walk
+            E = ((~x0 & ~x1) | (x0 & x1)) & 0xffffu;  // LEFT, or STOP (both bits)
+            if (G == -1) { D = 1; E = 1; }            // row 0: the border ends the walk (STOP)
         }
-        if (G < -1) { D = 0; E = 0; St = 0; }
+        if (G < -1) { D = 0; E = 0; }
         W[w] = window(E, D);
-        if constexpr (LOCAL) S[w] = spread16(St) << 1;
     });
 }
 
@@ -206,7 +202,7 @@ __device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_
 // at lane K, 0x100|K = STOP at lane K; lp = the last record written (or the STOP's p).
 template <bool LOCAL>
 __device__ __forceinline__ void walk_batch_asm(int &u, int &pa, int &na, int &st, int &lp, uint32_t &vrec,
-                                               uint32_t (&W)[8], uint32_t (&S)[8])
+                                               uint32_t (&W)[8])
 {
     if constexpr (!LOCAL)
     {
@@ -223,9 +219,7 @@ __device__ __forceinline__ void walk_batch_asm(int &u, int &pa, int &na, int &st
         asm volatile(SA_WALK_ROWS_LOCAL
                      : [u] "+s"(u), [pa] "+s"(pa), [na] "+s"(na), [st] "=&s"(st), [lp] "=&s"(lp), [rec] "+v"(vrec),
                        [w0] "+v"(W[0]), [w1] "+v"(W[1]), [w2] "+v"(W[2]), [w3] "+v"(W[3]), [w4] "+v"(W[4]),
-                       [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7]), [s0] "+v"(S[0]), [s1] "+v"(S[1]),
-                       [s2] "+v"(S[2]), [s3] "+v"(S[3]), [s4] "+v"(S[4]), [s5] "+v"(S[5]), [s6] "+v"(S[6]),
-                       [s7] "+v"(S[7])
+                       [w5] "+v"(W[5]), [w6] "+v"(W[6]), [w7] "+v"(W[7])
                      :
                      : "scc", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "s92", "s93", "s94", "s95",
                        "s96", "s97");
@@ -244,7 +238,7 @@ struct Lines {
 
 // The generic loop over lanes kk .. kmin (the asm's logic); `restage` refills exhausted windows.
 template <bool LOCAL, typename Restage>
-__device__ __forceinline__ void walk_lines(Lines &L, int kmin, uint32_t (&W)[8], uint32_t (&S)[8], Restage &&restage)
+__device__ __forceinline__ void walk_lines(Lines &L, int kmin, uint32_t (&W)[8], Restage &&restage)
 {
     while (L.kk >= kmin)
     {
@@ -258,18 +252,15 @@ __device__ __forceinline__ void walk_lines(Lines &L, int kmin, uint32_t (&W)[8],
             sfor<7>([&](auto Xc) {
                 constexpr int q = decltype(Xc)::value;
                 W[q] = W[q + 1];
-                if constexpr (LOCAL) S[q] = S[q + 1];
             });
             W[7] = 0;
-            if constexpr (LOCAL) S[7] = 0;
             ++L.na;
             continue;
         }
         const int pp = (int)__builtin_ctz((uint32_t)x);
         if constexpr (LOCAL)
         {
-            const uint32_t sw = (uint32_t)__builtin_amdgcn_readlane((int)S[0], L.kk);
-            if ((sw >> (L.u + pp)) & 1u)
+            if ((x >> (pp ^ 1)) & 1u)  // both bits: STOP
             {
                 L.stopped = true;
                 L.stopLane = L.kk;
@@ -288,13 +279,13 @@ __device__ __forceinline__ void walk_lines(Lines &L, int kmin, uint32_t (&W)[8],
 
 // The unrolled batch, then the generic loop for whatever it left (a restage or nothing).
 template <bool LOCAL, typename Restage>
-__device__ __forceinline__ void walk_batch(Lines &L, bool fast, int kmin, uint32_t (&W)[8], uint32_t (&S)[8],
+__device__ __forceinline__ void walk_batch(Lines &L, bool fast, int kmin, uint32_t (&W)[8],
                                            Restage &&restage)
 {
     if (fast && L.kk == 63 && kmin == 0)
     {
         int st, lp;
-        walk_batch_asm<LOCAL>(L.u, L.pa, L.na, st, lp, L.vrec, W, S);
+        walk_batch_asm<LOCAL>(L.u, L.pa, L.na, st, lp, L.vrec, W);
         if (st < 0)
         {
             L.kk = -1;
@@ -313,7 +304,7 @@ __device__ __forceinline__ void walk_batch(Lines &L, bool fast, int kmin, uint32
             }
         }
     }
-    walk_lines<LOCAL>(L, kmin, W, S, restage);
+    walk_lines<LOCAL>(L, kmin, W, restage);
 }
 
 // Start cell and score of pair p; false when there is nothing to walk (head complete).
@@ -399,20 +390,24 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
         Lines L;
         // expected column drift of the path per strip (prefetch placement)
         const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+        uint64_t tStage = 0, tBatch = 0;  // shader clocks in staging / in the walk proper
+#endif
         while (b >= 0)
         {
             const uint32_t *sb = mb + (int64_t)b * sstride;
             // this strip's prefetch has landed; the record store of the previous strip (issued
             // after it, the youngest vector-memory operation) may still be in flight
             asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            uint32_t W[8], S[8];
+            uint32_t W[8];
             int jo = jc;
-            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, S);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
+            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W);
             // the windows are complete before the prefetch below is issued: otherwise the wait for
             // the staging loads (vmcnt) would also wait for the prefetch
             asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
-            if constexpr (LOCAL)
-                asm volatile("" : "+v"(S[0]), "+v"(S[1]), "+v"(S[2]), "+v"(S[3]), "+v"(S[4]), "+v"(S[5]), "+v"(S[6]), "+v"(S[7]));
             int pfnext = INT_MIN;
             if (b > 0)
             {
@@ -437,9 +432,18 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
                 jo -= 16 * L.na;  // the eight windows are exhausted: the next 128 columns
                 L.na = 0;
                 L.u = 0;
-                rw_stage<LOCAL>(sb, pfbuf[pfb], INT_MIN, jo, lane, W, S);
+                rw_stage<LOCAL>(sb, pfbuf[pfb], INT_MIN, jo, lane, W);
             };
-            walk_batch<LOCAL>(L, a.fast != 0, 0, W, S, restage);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            asm volatile("" : "+v"(W[0]));
+            const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
+            walk_batch<LOCAL>(L, a.fast != 0, 0, W, restage);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            const uint64_t c2 = __builtin_amdgcn_s_memtime();
+            tStage += c1 - c0;
+            tBatch += c2 - c1;
+#endif
             // records of rows k .. kend (record index: rows walked before + k - lane)
             const int kend = L.stopped ? L.stopLane + 1 : 0;
             if (lane >= kend && lane <= k) rec[nrec + k - lane] = (int32_t)L.vrec;
@@ -470,6 +474,13 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
             pfclo = pfnext;
         }
         h.nrec = nrec;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+        if (a.timing && lane == 0)
+        {
+            a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p] = tStage;
+            a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p + 1] = tBatch;
+        }
+#endif
         if (!L.stopped)
         {
             if constexpr (!LOCAL)
@@ -525,8 +536,8 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
         L.u = 2 * (16 * G0 + 16 - i);
         while (J0 >= 1)
         {
-            uint32_t W[8], S[8];
-            cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W, S);
+            uint32_t W[8];
+            cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
             const int kmin = max(0, 64 - J0);  // lanes of columns >= 1
             L.pa = 0;
             L.na = 0;
@@ -536,9 +547,9 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
                 G0 -= L.na;  // the eight blocks are exhausted: the next eight above
                 L.na = 0;
                 L.u = 0;
-                cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W, S);
+                cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
             };
-            walk_batch<LOCAL>(L, a.fast != 0, kmin, W, S, restage);
+            walk_batch<LOCAL>(L, a.fast != 0, kmin, W, restage);
             const int kend = L.stopped ? L.stopLane + 1 : kmin;
             if (lane >= kend) rec[nrec + 63 - lane] = (int32_t)L.vrec;
             nrec += 64 - kend;

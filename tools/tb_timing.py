@@ -30,6 +30,10 @@ b.traceback()  # the file holds the last call's timestamps
 r = b.results()[0]
 tm = np.fromfile(path, dtype=np.uint64).astype(np.int64)
 walk_us = (tm[1] - tm[0]) * 0.01
-print({"n": args.n, "m": args.m, "mode": args.mode, "ops": r["num_bytes"], "walk_us": round(walk_us, 1),
-       "walk_ns_per_op": round(walk_us * 1000 / max(1, r["num_bytes"]), 2)})
+rec = {"n": args.n, "m": args.m, "mode": args.mode, "ops": r["num_bytes"], "walk_us": round(walk_us, 1),
+       "walk_ns_per_op": round(walk_us * 1000 / max(1, r["num_bytes"]), 2)}
+if len(tm) >= 4 and tm[2] > 0:
+    # experiment builds with SA_EXP_WALK_TIMING: shader clocks in staging / in the row walk proper
+    rec.update({"stage_clk_per_row": round(tm[2] / args.m, 1), "batch_clk_per_row": round(tm[3] / args.m, 1)})
+print(rec)
 b.close()
