@@ -23,8 +23,9 @@ One step (roles rotate A -> B -> C every step; F alternates between two register
     i/j/k  push the sign bits into the plane words (v_alignbit acc, acc, t, 31)
 The next step uses Q = B (old Qn), Qn = C, diag = A (this step's up).
 
-Local keys: key' = (F' << kb) - q, its running maximum bm over the block; the caller adds the
-body's key base (kmask - (s0 & kmask)) once per body. Same order as the C++ recurrence
+Local keys: key' = (F' << kb) - q, its running maximum bm over the block (one v_max3 per two
+steps: keys alternate between two registers); the caller adds the body's key base
+(kmask - (s0 & kmask)) once per body. Same order as the C++ recurrence
 (alignSequenceCPU.cpp:175-192): larger H first, then the earlier column.
 """
 import os
@@ -48,14 +49,14 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     # raw tag, the sign-bit constant). A raw tag is (c + 63) << 20 of the slot's column c: its bit 31 is
     # the lap parity, the complement of the tag (sa_fill.hip ring_tag); v_bitop3 applies it.
     h = 2 if hp else 0
-    nout = (11 if not local else 16) + h
+    nout = (11 if not local else 17) + h
     PF = f"%{nout - 2}"
     BAD = f"%{nout - 1}"
     TW = [f"%{nout + i}" for i in range(4)]
     k = nout + 4
-    ACC2 = BM = X = T2 = KEY = G = KB = None
+    ACC2 = BM = X = T2 = KEY = KEY2 = G = KB = None
     if local:
-        ACC2, BM, X, T2, KEY = "%11", "%12", "%13", "%14", "%15"
+        ACC2, BM, X, T2, KEY, KEY2 = "%11", "%12", "%13", "%14", "%15", "%16"
         G, KB = f"%{k}", f"%{k + 1}"
         k += 2
     PFA, CTAG = f"%{k}", f"%{k + 1}"
@@ -99,11 +100,13 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
             out.append(f"v_sub_u32_e64 {fn}, {X}, {G} clamp")
             out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
             out.append(f"v_add_u32_e32 {T2}, -1, {fn}")
-            out.append(f"v_lshl_add_u32 {KEY}, {fn}, {KB}, {-q}")
+            kreg = KEY if k % 2 == 0 else KEY2
+            out.append(f"v_lshl_add_u32 {kreg}, {fn}, {KB}, {-q}")
             if hn and not last:
                 out.append(f"v_mov_b32_e32 {c}, {fn}")
             out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
-            out.append(f"v_max_i32_e32 {BM}, {BM}, {KEY}")
+            if k % 2 == 1:
+                out.append(f"v_max3_i32 {BM}, {BM}, {KEY}, {KEY2}")
             out.append(f"v_alignbit_b32 {ACC2}, {ACC2}, {T2}, 31")
         roles = [b, c, a]
     if hp:
@@ -144,12 +147,12 @@ def main():
                 lines.append(f"template <> __device__ __forceinline__ void steps_asm<{str(local).lower()}, "
                              f"{str(hn).lower()}, {str(hp).lower()}>(StepRegs &r)")
                 lines.append("{")
-                lines.append("    int D, M, t0, t1, X, t2, key;")
+                lines.append("    int D, M, t0, t1, X, t2, key, key2;")
                 lines.append(f"    asm volatile(\"{body}\"")
                 lines.append("        : \"+v\"(r.Q), \"=&v\"(r.Qn), \"+v\"(r.diag), \"+v\"(r.F), \"=&v\"(r.F2),")
                 lines.append("          \"=&v\"(D), \"=&v\"(M), \"=&v\"(t0), \"=&v\"(t1), \"+v\"(r.acc0), \"+v\"(r.acc1)")
                 if local:
-                    lines.append("          , \"+v\"(r.acc2), \"+v\"(r.bm), \"=&v\"(X), \"=&v\"(t2), \"=&v\"(key)")
+                    lines.append("          , \"+v\"(r.acc2), \"+v\"(r.bm), \"=&v\"(X), \"=&v\"(t2), \"=&v\"(key), \"=&v\"(key2)")
                 if hp:
                     # early-clobber: the mask is written before the publish reads its raw tag (an SGPR
                     # input the compiler could otherwise assign to the same register)
@@ -164,7 +167,7 @@ def main():
                 if hn or hp:
                     ins += ", \"v\"(r.msb)"
                 lines.append(f"        : {ins}" + (" : \"scc\");" if hp else ");"))
-                lines.append("    (void)D; (void)M; (void)t0; (void)t1; (void)X; (void)t2; (void)key;")
+                lines.append("    (void)D; (void)M; (void)t0; (void)t1; (void)X; (void)t2; (void)key; (void)key2;")
                 lines.append(f"    r.rotate<{rot(U)}>();")
                 lines.append("}")
                 lines.append("")
