@@ -999,34 +999,24 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int 
     for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
     {
         bool moved = false;
+        // 1. issue the granule poll (not waited for yet: the drain below runs under its latency, so
+        //    the outgoing bottom row does not wait a global round trip per iteration)
+        int want = 0;
+        uint64_t v = 0;
         if (copied < nIn)
         {
             // ring[0]'s consumer publishes its consumption every kConsEvery columns
             const int room = uniform(lds_ld(cons0)) + kRing - copied;  // free ring slots
-            const int want = min(min(kWave, nIn - copied), room);
+            want = min(min(kWave, nIn - copied), room);
             if (want >= min(16, nIn - copied))
-            {
                 // every poll loads the whole window (one round trip from the producer's store to
                 // the ring; a lane-0 probe first would add a second): 512 bytes per poll per waiting
                 // group is nothing next to the fill's own traffic
-                const uint64_t v = lane < want ? load_granule(bin + copied + lane) : 0;
-                const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
-                const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
-                if (cnt >= min(16, nIn - copied))
-                {
-                    const int c = copied + lane + 1;
-                    if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
-                    // I/O progress stamps: when ring[0] got column 4096q (timeline words 16..25 of
-                    // the group's first strip)
-                    if (a.timeline && lane == 0 && ((copied + cnt) >> 12) != (copied >> 12) && ((copied + cnt) >> 12) < 10)
-                        a.timeline[kTimelineWords * (size_t)first + 16 + ((copied + cnt) >> 12)] = now_ticks();
-#endif
-                    copied += cnt;
-                    moved = true;
-                }
-            }
+                v = lane < want ? load_granule(bin + copied + lane) : 0;
+            else
+                want = 0;
         }
+        // 2. drain ring[W'] into granules for the next group
         if (drained < nOut)
         {
             const int c = drained + lane + 1;
@@ -1038,6 +1028,25 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int 
                 if (c <= upto) store_granule(bout + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
                 drained = upto;
                 if (lane == 0) lds_st(consL, drained);
+                moved = true;
+            }
+        }
+        // 3. the poll's result -> ring[0]
+        if (want > 0)
+        {
+            const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
+            const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
+            if (cnt >= min(16, nIn - copied))
+            {
+                const int c = copied + lane + 1;
+                if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
+                // I/O progress stamps: when ring[0] got column 4096q (timeline words 16..25 of
+                // the group's first strip)
+                if (a.timeline && lane == 0 && ((copied + cnt) >> 12) != (copied >> 12) && ((copied + cnt) >> 12) < 10)
+                    a.timeline[kTimelineWords * (size_t)first + 16 + ((copied + cnt) >> 12)] = now_ticks();
+#endif
+                copied += cnt;
                 moved = true;
             }
         }
