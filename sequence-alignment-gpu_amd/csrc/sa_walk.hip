@@ -534,10 +534,20 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
         int nrec = 0;
         Lines L;
         L.u = 2 * (16 * G0 + 16 - i);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+        uint64_t tStage = 0, tBatch = 0;
+#endif
         while (J0 >= 1)
         {
             uint32_t W[8];
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            const uint64_t c0 = __builtin_amdgcn_s_memtime();
+#endif
             cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            asm volatile("" : "+v"(W[0]), "+v"(W[7]));
+            const uint64_t c1 = __builtin_amdgcn_s_memtime();
+#endif
             const int kmin = max(0, 64 - J0);  // lanes of columns >= 1
             L.pa = 0;
             L.na = 0;
@@ -550,6 +560,11 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
                 cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
             };
             walk_batch<LOCAL>(L, a.fast != 0, kmin, W, restage);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            const uint64_t c2 = __builtin_amdgcn_s_memtime();
+            tStage += c1 - c0;
+            tBatch += c2 - c1;
+#endif
             const int kend = L.stopped ? L.stopLane + 1 : kmin;
             if (lane >= kend) rec[nrec + 63 - lane] = (int32_t)L.vrec;
             nrec += 64 - kend;
@@ -576,6 +591,13 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
             J0 -= 64;
         }
         h.nrec = nrec;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+        if (a.timing && lane == 0)
+        {
+            a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p] = tStage;
+            a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p + 1] = tBatch;
+        }
+#endif
         if (!L.stopped)
         {
             const int icur = 16 * G0 + 16 - (L.u >> 1);  // row after the move into column 0 (0: row 0)
