@@ -195,6 +195,72 @@ __device__ __forceinline__ void cw_stage(const uint32_t *__restrict__ mb, int64_
     });
 }
 
+// Column walk, R = 32, one strip per pair (the batch shapes), staged from an LDS copy of the plane
+// sectors the next batch will need: the gathers of cw_stage (16 chunks x one 32-B strip-lane sector
+// per window, for 64 columns) were latency-bound with every pair of a batch in flight (255 clk per
+// column against 21 alone, tools/tb_batch_phase.py), so they are issued a batch ahead with
+// global_load_lds. Buffer layout: [chunk - c_lo][k - k_lo][8 dwords] (a strip lane's segment of a
+// chunk: 4 words per plane), kCwChunks x kCwLanes entries.
+constexpr int kCwChunks = 20, kCwLanes = 8;  // 64 columns + 8 lanes of skew span <= 19 chunks
+constexpr int kCwDw = kCwChunks * kCwLanes * 8;
+
+// The k range [k_lo, k_lo + kCwLanes) that should cover the next batch's windows when the path
+// moves `drift` row blocks per batch (rows blocks G0' - 7 .. G0', k = G >> 1).
+__device__ __forceinline__ int cw_klo(int G0, int drift) { return max(0, ((G0 - drift - 7) >> 1) - 1); }
+
+// Prefetch for the batch whose lane 63 is column J0n: chunks from the first step it reads.
+__device__ __forceinline__ void cw_prefetch(const uint32_t *__restrict__ mb, int nchunks, int J0n, int klo, int lane,
+                                            uint32_t *buf, int &clo)
+{
+    clo = max(0, (J0n - 64 + klo) >> 2);  // step s = j - 1 + k of column J0n - 63 and lane k_lo
+    sfor<kCwChunks * kCwLanes * 2 / kWave>([&](auto Ic) {
+        constexpr int it = decltype(Ic)::value;
+        const int q = it * kWave + lane;        // 16-B piece: (chunk, lane, half)
+        const int c = min(clo + (q >> 4), nchunks - 1);
+        const int k = min(klo + ((q >> 1) & 7), kWave - 1);
+        const uint32_t *src = mb + (int64_t)c * (kWave * 8) + k * 8 + (q & 1) * 4;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)src,
+                                         (__attribute__((address_space(3))) void *)(buf + it * kWave * 4), 16, 0, 0);
+    });
+}
+
+// cw_stage for R = 32 reading the LDS copy (the caller has checked that it covers the windows)
+template <bool LOCAL>
+__device__ __forceinline__ void cw_stage_lds(const uint32_t *buf, int clo, int klo, int J0, int G0, int lane,
+                                             uint32_t (&W)[8])
+{
+    const int j = J0 - 63 + lane;
+    sfor<8>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        const int G = G0 - w;  // uniform
+        uint32_t x0 = 0, x1 = 0;
+        if (G >= 0)
+        {
+            const int k = G >> 1, sh = 16 - 16 * (G & 1);  // rho0 = 16 (G & 1)
+            const int s = max(j - 1 + k, 0);
+            // (lanes left of column 1 compute an index outside the copy: clamped, value unused)
+            const int ix = min(max((((s >> 2) - clo) * kCwLanes + (k - klo)) * 8 + (s & 3), 0), kCwDw - 8);
+            x0 = j >= 1 ? (buf[ix] >> sh) & 0xffffu : 0u;
+            x1 = j >= 1 ? (buf[ix + 4] >> sh) & 0xffffu : 0u;
+        }
+        uint32_t E, D;
+        if constexpr (!LOCAL)
+        {
+            D = x0;
+            E = ~x0 & ~x1 & 0xffffu;
+            if (G == -1) E = 1;
+        }
+        else
+        {
+            D = x0;
+            E = ((~x0 & ~x1) | (x0 & x1)) & 0xffffu;
+            if (G == -1) { D = 1; E = 1; }
+        }
+        if (G < -1) { D = 0; E = 0; }
+        W[w] = window(E, D);
+    });
+}
+
 // ------------------------------------------------------------------------------------------------
 // the walk
 // ------------------------------------------------------------------------------------------------
@@ -512,6 +578,7 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
 template <int R, bool LOCAL>
 __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 {
+    __shared__ uint32_t cwbuf[R == 32 ? 2 * kCwDw : 1];
     const int p = blockIdx.x;
     const int lane = threadIdx.x;
     PairDesc pd = a.pairs[p];
@@ -534,6 +601,11 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
         int nrec = 0;
         Lines L;
         L.u = 2 * (16 * G0 + 16 - i);
+        // R = 32 single-strip pairs: staging from the LDS copy issued one batch ahead
+        const bool useLds = R == 32 && nstrips == 1;
+        const int nchunks = (nsteps * R) / Geo<R>::CS;
+        const int drift = (int)(((int64_t)m * 64 + n / 2) / max(n, 1) / 16);  // row blocks per batch
+        int pfb = 0, pfclo = -1, pfklo = 0, pfJ0 = INT_MIN;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
         uint64_t tStage = 0, tBatch = 0;
 #endif
@@ -543,7 +615,27 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
-            cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
+            bool fromLds = false;
+            if constexpr (R == 32)
+            {
+                // the copy for this batch has landed (the previous batch's record store, issued after
+                // it, may still be in flight)
+                asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                const int kHi = max(G0, 0) >> 1, kLo = max(G0 - 7, 0) >> 1;
+                fromLds = useLds && pfJ0 == J0 && kLo >= pfklo && kHi < pfklo + kCwLanes;
+                if (fromLds) cw_stage_lds<LOCAL>(cwbuf + pfb * kCwDw, pfclo, pfklo, J0, G0, lane, W);
+            }
+            if (!fromLds) cw_stage<R, LOCAL>(mb, sstride, J0, G0, lane, W);
+            // the windows are complete before the next prefetch is issued (its wait must not cover them)
+            asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
+            if constexpr (R == 32)
+                if (useLds && J0 > 64)
+                {
+                    pfb ^= 1;
+                    pfklo = cw_klo(G0, drift);
+                    pfJ0 = J0 - 64;
+                    cw_prefetch(mb, nchunks, pfJ0, pfklo, lane, cwbuf + pfb * kCwDw, pfclo);
+                }
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             asm volatile("" : "+v"(W[0]), "+v"(W[7]));
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
