@@ -276,3 +276,50 @@ def test_local_best_cell_near_last_column(eng, gap):
             got = eng.align_pair(1, t, pp, S, gap, rows_per_lane=1)
             got.pop("fill_us")
             assert got == exp, (n, len(pp), gap)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_low_complexity_and_extreme_shapes(eng, mode):
+    """Inputs whose direction matrices are all ties or long single-direction runs: homopolymers,
+    period-4 repeats against a shifted copy, a 20000-column text against a 70-row pattern (LEFT runs
+    thousands of columns long), a 9000-row pattern against a 300-column text (UP runs), and a text
+    and pattern with no letter in common (local score 0). Every strip height the planner picks plus
+    R = 1 and 32, bit-exact vs the oracle."""
+    S = synthetic.blast_matrix()
+    A, C, G, T = 0, 2, 3, 1  # "ATCG" codes
+    rep = np.array([A, C, G, T], np.int8)
+    cases = [
+        (np.full(5000, A, np.int8), np.full(3000, A, np.int8)),
+        (np.tile(rep, 1500), np.tile(np.roll(rep, 1), 1100)),
+        (synthetic.random_sequence(1700, 20000, 4), synthetic.random_sequence(1701, 70, 4)),
+        (synthetic.random_sequence(1702, 300, 4), synthetic.random_sequence(1703, 9000, 4)),
+        (np.tile(np.array([A, T], np.int8), 2100), np.tile(np.array([C, G], np.int8), 1900)),
+    ]
+    for k, (t, p) in enumerate(cases):
+        exp = oracle.align(mode, t, p, S, 5)
+        for R in (0, 1, 32):
+            got = eng.align_pair(mode, t, p, S, 5, rows_per_lane=R)
+            got.pop("fill_us")
+            assert got == exp, (k, len(t), len(p), R)
+
+
+@pytest.mark.parametrize("rows_per_lane", [0, 16, 32])
+def test_low_complexity_batch(eng, rows_per_lane):
+    """The same all-tie and long-run inputs through one plan of equal-shape pairs (the pair-packed
+    fill for global at R = 16/32, the batch column walk at R = 32): every pair bit-exact."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    rep = np.array([0, 2, 3, 1], np.int8)
+    n, m = 2000, 1800
+    texts = [np.full(n, 0, np.int8), np.tile(rep, n // 4), np.tile(rep, n // 4),
+             np.tile(np.array([0, 1], np.int8), n // 2)]
+    pats = [np.full(m, 0, np.int8), np.tile(np.roll(rep, 1), m // 4), np.full(m, 3, np.int8),
+            np.tile(np.array([2, 3], np.int8), m // 2)]
+    for mode in (0, 1):
+        b = DeviceBatch(mode, S, 5, texts, pats, rows_per_lane=rows_per_lane)
+        b.fill()
+        b.traceback()
+        got = b.all_alignments()
+        b.close()
+        for k in range(len(texts)):
+            assert got[k] == oracle.align(mode, texts[k], pats[k], S, 5), (mode, k)
