@@ -4,7 +4,8 @@ oracle otherwise), and out-of-alphabet input bytes.
 
 CPU: the oracle reproduces every record. GPU: one-shot at several strip heights, one plan mixing
 empty and non-empty pairs, sa_align_batch over two shards; a plan whose arena holds a byte outside
-0..A-1 reports SA_ERR_INVALID instead of a silently clamped alignment.
+0..A-1 reports SA_ERR_INVALID instead of a silently clamped alignment, and so does the one-shot
+path (flagged on the device by its encode kernel; there is no host scan of the inputs).
 """
 from __future__ import annotations
 
@@ -79,7 +80,7 @@ def test_out_of_alphabet_bytes_are_rejected(eng, where):
     p = synthetic.random_sequence(6, 200, 4)
     (t if where == "text" else p)[17] = 4  # one byte past the DNA alphabet
     with pytest.raises(eng.SaError):
-        eng.align_pair(0, t, p, S, 5)  # host-side check of the one-shot path
+        eng.align_pair(0, t, p, S, 5)  # the one-shot path's encode kernel flags it (ctrl.bad_input)
     b = DeviceBatch(0, S, 5, [synthetic.random_sequence(7, 100, 4), t], [synthetic.random_sequence(8, 90, 4), p])
     b.fill()
     b.traceback()
