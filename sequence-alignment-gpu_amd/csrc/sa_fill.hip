@@ -793,9 +793,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
 //     rA | 0x0c00 | (4 + rB) << 16 | 0x0c000000, and one v_perm_b32(colB, colA, sel) gives the row's
 //     two scores as u16 halves.
 //   * Direction bits: slot σ of a 16-slot group sits at bit 15 - σ of each half. Slots s and s+8
-//     (s < 8) are rows ρ and ρ+8 of the same step (R >= 16); one v_perm_b32 gathers the four sign
-//     bits (both pairs, both slots) onto byte MSBs (bits 15, 7, 31, 23), one shift by s moves them to
-//     15-s, 7-s, 31-s, 23-s, and one v_and_or_b32 inserts them: 3 VALU per 4 bits.
+//     (s < 8) are rows ρ and ρ+8 of the same step (R >= 16); one v_perm_b32 spreads the four sign
+//     bits (both pairs, both slots) over whole bytes (sign-replicating selectors), and one
+//     v_bfi_b32 keeps bits 15-s, 7-s, 31-s, 23-s of them: 2 VALU per 4 bits (was 3 with a shift).
 //   * At the body's end v_perm_b32 splits the packed words back into each pair's ordinary 32-slot
 //     words, so the stored planes, the traceback and the decoders are exactly those of the unpacked
 //     kernel.
@@ -883,22 +883,26 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
                 F[rho] = Fn;
                 // rows rho-8 and rho of a 16-row group are slots s and s+8 of packed word w: insert
                 // as soon as both exist (keeps at most 8 rows of differences live)
+                // perm selectors 8..11 replicate the sign bit of a 16-bit half over a whole byte, so
+                // the four signs arrive as 0x00 / 0xff bytes and one bit-field insert puts them at
+                // 7 - sl of each byte, no shift: 2 VALU per 4 bits. Slot sl = 0 keeps the whole bytes;
+                // slots 1..7 overwrite their low bits.
                 if constexpr (rho % 16 >= 8)
                 {
                     constexpr int sl = rho % 16 - 8;
                     constexpr int w = (q * R + rho) / 16;
                     constexpr uint32_t mask = (0x80808080u >> sl);
-                    const uint32_t y0 = __builtin_amdgcn_perm(x0[rho - 8], x0[rho], 0x07030501u) >> sl;
-                    const uint32_t y1 = __builtin_amdgcn_perm(x1[rho - 8], x1[rho], 0x07030501u) >> sl;
+                    const uint32_t y0 = __builtin_amdgcn_perm(x0[rho - 8], x0[rho], 0x0b090a08u);
+                    const uint32_t y1 = __builtin_amdgcn_perm(x1[rho - 8], x1[rho], 0x0b090a08u);
                     if constexpr (sl == 0)
                     {
-                        acc[0][w] = y0 & mask;
-                        acc[1][w] = y1 & mask;
+                        acc[0][w] = y0;
+                        acc[1][w] = y1;
                     }
                     else
                     {
-                        acc[0][w] |= y0 & mask;
-                        acc[1][w] |= y1 & mask;
+                        asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(acc[0][w]) : "v"(mask), "v"(y0));
+                        asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(acc[1][w]) : "v"(mask), "v"(y1));
                     }
                 }
             });
