@@ -289,7 +289,10 @@ def main():
     launch_ms = [a.elapsed_time(b) for a, b in evs]
     res = job.results()  # checks the abort flag of the last fill
 
-    # traceback / end-to-end, outside the timed region (headline: reported only)
+    # traceback / end-to-end, outside the timed region (headline: reported only); one untimed pass
+    # first, so the traceback kernels' first launch in the process (code object load) is not timed
+    if args.workload != "batch":
+        job.fill_and_traceback()
     torch.cuda.synchronize(local)
     e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
     job.fill_and_traceback((e0, e1))

@@ -722,12 +722,17 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 // expansion: records -> aligned strings (forward order) and the per-pair result
 // ------------------------------------------------------------------------------------------------
 // Grid (chunks, pairs): block c of a pair expands records [c * kChunkRecs, (c+1) * kChunkRecs), so a
-// single long pair spreads over up to kMaxChunks CUs (one workgroup took 0.18 ms at 32768^2). Each
-// block first sums every record of the pair (the total length L fixes the forward positions) and
-// those before its chunk (its starting position and letter counts) in one strided pass — O(N) reads
-// per block, served by L2 — then scans its own records. Block 0 also writes the trailing run and
-// the sa_result.
+// single long pair spreads over up to kMaxChunks CUs (one workgroup took 0.18 ms at 32768^2). A block
+// whose chunk is not the whole pair first sums every record of the pair (the total length L fixes the
+// forward positions) and those before its chunk (its starting position and letter counts) in one
+// strided pass — O(N) reads per block, served by L2; a block holding all of its pair's records (the
+// batch: one chunk per pair) takes the totals from its own scan. Each thread expands a run of
+// consecutive records; their letters go to an LDS copy of the chunk's slice of both strings when it
+// fits (kStage bytes each), which the block then writes out in aligned dwords (per-thread byte runs
+// land ~10 bytes apart, one uncoalesced byte store per letter), else straight to HBM. Block 0 also
+// writes the trailing run and the sa_result.
 constexpr int kExpThreads = 256;
+constexpr int kStage = 12288;  // LDS staging bytes per string
 
 // block-wide sums of two 64-bit values (tree in LDS)
 __device__ __forceinline__ void block_sum2(int64_t &x, int64_t &y, int64_t *lds)
@@ -750,67 +755,39 @@ __device__ __forceinline__ void block_sum2(int64_t &x, int64_t &y, int64_t *lds)
     __syncthreads();
 }
 
+// exclusive block scan: inclusive scan inside each wave by lane shifts, then the waves' totals
 __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t *lds, int64_t &total)
 {
-    const int t = threadIdx.x;
-    lds[t] = v;
-    __syncthreads();
-    for (int d = 1; d < kExpThreads; d <<= 1)
+    const int t = threadIdx.x, lane = t & (kWave - 1), wv = t / kWave;
+    int64_t x = v;
+    for (int d = 1; d < kWave; d <<= 1)
     {
-        const int64_t x = t >= d ? lds[t - d] : 0;
-        __syncthreads();
-        lds[t] += x;
-        __syncthreads();
+        const int64_t y = __shfl_up(x, d, kWave);
+        if (lane >= d) x += y;
     }
-    total = lds[kExpThreads - 1];
-    const int64_t incl = lds[t];
+    if (lane == kWave - 1) lds[wv] = x;
     __syncthreads();
-    return incl - v;
+    int64_t before = 0;
+    total = 0;
+    for (int k = 0; k < kExpThreads / kWave; ++k)
+    {
+        const int64_t s = lds[k];
+        before += k < wv ? s : 0;
+        total += s;
+    }
+    __syncthreads();
+    return before + x - v;
 }
 
 // ops and letters consumed along the free coordinate by record v, packed (each < 2^31 per pair)
 __device__ __forceinline__ int64_t rec_counts(int v) { return ((int64_t)((v >> 1) + 1) << 32) | (int64_t)((v >> 1) + (v & 1)); }
 
-__global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
+// records [lo, hi) of a pair -> put(forward position, text letter, pattern letter)
+template <class Put>
+__device__ __forceinline__ void expand_records(const TbHead &h, const int32_t *rec, int lo, int hi, int64_t P,
+                                               int64_t C0, int64_t L, const int8_t *tx, const int8_t *px,
+                                               const char *alpha, char GAP, Put put)
 {
-    __shared__ int64_t scan[2 * kExpThreads];
-    __shared__ char alpha[40];
-    const int p = blockIdx.y;
-    const int t = threadIdx.x;
-    const TbHead h = a.heads[p];
-    const int N = h.nrec;
-    const int c0 = (int)blockIdx.x * a.chunk_recs;
-    if (blockIdx.x > 0 && c0 >= N) return;  // (uniform per block)
-    if (t < 33) alpha[t] = a.alphabet[t];
-    const PairDesc pd = a.pairs[p];
-    const int32_t *rec = a.rec + pd.rec_off;
-    const int8_t *tx = a.text + pd.text_off;
-    const int8_t *px = a.pattern + pd.pattern_off;
-    char *ot = a.out_text + pd.out_off;
-    char *op = a.out_pattern + pd.out_off;
-    const int cend = min(N, c0 + a.chunk_recs);
-    // pass 0: totals over the pair and the prefix before this chunk
-    int64_t tot = 0, pre = 0;
-    for (int q = t; q < N; q += kExpThreads)
-    {
-        const int64_t x = rec_counts(rec[q]);
-        tot += x;
-        pre += q < c0 ? x : 0;
-    }
-    block_sum2(tot, pre, scan);
-    const int64_t totCnt = tot >> 32, totCons = tot & 0xffffffffll;
-    // pass 1: this thread's records of the chunk
-    const int per = (cend - c0 + kExpThreads - 1) / kExpThreads;
-    const int lo = min(cend, c0 + t * per), hi = min(cend, lo + per);
-    int64_t mine = 0;
-    for (int q = lo; q < hi; ++q) mine += rec_counts(rec[q]);
-    int64_t chunkTot;
-    const int64_t ex = block_exclusive_scan(mine, scan, chunkTot) + pre;
-    const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
-    const int64_t L = totCnt + h.tail;
-    const char GAP = alpha[a.A];
-    // pass 2
-    int64_t P = P0;
     if (h.kind == kRecRows)
     {
         // record q: row i0 - q entered at column j; `run` LEFTs, then DIAG (to column j - run - 1) or TOP
@@ -821,13 +798,8 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
             const int run = v >> 1, d = v & 1;
             const int64_t flo = L - 1 - P - run;  // forward position of the leaving move
             const int64_t jl = j - run;           // column of the leaving cell
-            ot[flo] = d ? alpha[tx[jl - 1]] : GAP;
-            op[flo] = alpha[px[i - 1]];
-            for (int r = 0; r < run; ++r)
-            {
-                ot[flo + 1 + r] = alpha[tx[jl + r]];
-                op[flo + 1 + r] = GAP;
-            }
+            put(flo, d ? alpha[tx[jl - 1]] : GAP, alpha[px[i - 1]]);
+            for (int r = 0; r < run; ++r) put(flo + 1 + r, alpha[tx[jl + r]], GAP);
             P += run + 1;
             j = jl - d;
             i -= 1;
@@ -843,17 +815,98 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
             const int run = v >> 1, d = v & 1;
             const int64_t flo = L - 1 - P - run;
             const int64_t il = i - run;  // row of the leaving cell
-            ot[flo] = alpha[tx[j - 1]];
-            op[flo] = d ? alpha[px[il - 1]] : GAP;
-            for (int r = 0; r < run; ++r)
-            {
-                ot[flo + 1 + r] = GAP;
-                op[flo + 1 + r] = alpha[px[il + r]];
-            }
+            put(flo, alpha[tx[j - 1]], d ? alpha[px[il - 1]] : GAP);
+            for (int r = 0; r < run; ++r) put(flo + 1 + r, GAP, alpha[px[il + r]]);
             P += run + 1;
             i = il - d;
             j -= 1;
         }
+    }
+}
+
+__global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
+{
+    __shared__ int64_t scan[2 * kExpThreads];
+    __shared__ char alpha[40];
+    __shared__ __attribute__((aligned(16))) char stT[kStage], stP[kStage];
+    const int p = blockIdx.y;
+    const int t = threadIdx.x;
+    const TbHead h = a.heads[p];
+    const int N = h.nrec;
+    const int c0 = (int)blockIdx.x * a.chunk_recs;
+    if (blockIdx.x > 0 && c0 >= N) return;  // (uniform per block)
+    if (t < 33) alpha[t] = a.alphabet[t];
+    const PairDesc pd = a.pairs[p];
+    const int32_t *rec = a.rec + pd.rec_off;
+    const int8_t *tx = a.text + pd.text_off;
+    const int8_t *px = a.pattern + pd.pattern_off;
+    char *ot = a.out_text + pd.out_off;
+    char *op = a.out_pattern + pd.out_off;
+    const int cend = min(N, c0 + a.chunk_recs);
+    const bool whole = c0 == 0 && cend == N;  // (uniform per block)
+    // pass 0 (chunks of a longer pair): totals over the pair and the prefix before this chunk
+    int64_t tot = 0, pre = 0;
+    if (!whole)
+    {
+        for (int q = t; q < N; q += kExpThreads)
+        {
+            const int64_t x = rec_counts(rec[q]);
+            tot += x;
+            pre += q < c0 ? x : 0;
+        }
+        block_sum2(tot, pre, scan);
+    }
+    // pass 1: this thread's records of the chunk
+    const int per = (cend - c0 + kExpThreads - 1) / kExpThreads;
+    const int lo = min(cend, c0 + t * per), hi = min(cend, lo + per);
+    int64_t mine = 0;
+    for (int q = lo; q < hi; ++q) mine += rec_counts(rec[q]);
+    int64_t chunkTot;
+    const int64_t ex = block_exclusive_scan(mine, scan, chunkTot) + pre;
+    if (whole) tot = chunkTot;
+    const int64_t totCnt = tot >> 32, totCons = tot & 0xffffffffll;
+    const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
+    const int64_t L = totCnt + h.tail;
+    const char GAP = alpha[a.A];
+    // pass 2: the chunk's forward positions are [L - (pre + chunk ops), L - pre); the LDS copy starts
+    // at the dword holding the first one, so LDS and HBM dwords line up
+    const int64_t fEnd = L - (pre >> 32);
+    const int64_t fBeg = fEnd - (chunkTot >> 32);
+    const int64_t sBeg = fBeg - (int64_t)(((uintptr_t)(ot + fBeg)) & 3);
+    const bool alignedTP = (((uintptr_t)ot ^ (uintptr_t)op) & 3) == 0;
+    if (alignedTP && fEnd - sBeg <= kStage)
+    {
+        expand_records(h, rec, lo, hi, P0, C0, L, tx, px, alpha, GAP, [&](int64_t f, char ct, char cp) {
+            stT[f - sBeg] = ct;
+            stP[f - sBeg] = cp;
+        });
+        __syncthreads();
+        // head bytes up to the first whole dword, whole dwords, tail bytes
+        const int64_t dBeg = (fBeg + 3 - sBeg) / 4, dEnd = (fEnd - sBeg) / 4;
+        const int64_t head = min(fEnd, sBeg + 4 * dBeg) - fBeg;
+        if (t < head)
+        {
+            ot[fBeg + t] = stT[fBeg - sBeg + t];
+            op[fBeg + t] = stP[fBeg - sBeg + t];
+        }
+        for (int64_t d = dBeg + t; d < dEnd; d += kExpThreads)
+        {
+            *reinterpret_cast<uint32_t *>(ot + sBeg + 4 * d) = *reinterpret_cast<const uint32_t *>(stT + 4 * d);
+            *reinterpret_cast<uint32_t *>(op + sBeg + 4 * d) = *reinterpret_cast<const uint32_t *>(stP + 4 * d);
+        }
+        const int64_t tBeg = max(fBeg + head, sBeg + 4 * dEnd);
+        if (tBeg + t < fEnd)
+        {
+            ot[tBeg + t] = stT[tBeg - sBeg + t];
+            op[tBeg + t] = stP[tBeg - sBeg + t];
+        }
+    }
+    else
+    {
+        expand_records(h, rec, lo, hi, P0, C0, L, tx, px, alpha, GAP, [&](int64_t f, char ct, char cp) {
+            ot[f] = ct;
+            op[f] = cp;
+        });
     }
     if (blockIdx.x != 0) return;
     // the trailing run: forward positions 0 .. tail-1, ending at the walk's last cell
