@@ -56,24 +56,29 @@ __global__ void encode_text_kernel(const int8_t *text, const int8_t *pattern, co
     {
         // selectors of pairs (2q, 2q+1) in pair 2q's block, padding included (0x0c0c0c0c = zeros)
         if ((blockIdx.y & 1) != 0) return;
+        // the column profile of each letter t (byte r = S[r][t] + 2g; A <= 4) from LDS, both pairs'
+        // columns in one 8-byte store
+        __shared__ uint32_t prof[4];
+        if (threadIdx.x < (unsigned)A)
+        {
+            uint32_t c = 0;
+            for (int r = 0; r < A; ++r) c |= ((uint32_t)table[r * A + threadIdx.x] & 0xffu) << (8 * r);
+            prof[threadIdx.x] = c;
+        }
+        __syncthreads();
         const PairDesc pb = pairs[blockIdx.y + 1];
+        uint2 *col = reinterpret_cast<uint2 *>(codes + pd.code_off);
         for (uint64_t xx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; xx < pd.code_len;
              xx += (uint64_t)gridDim.x * blockDim.x)
         {
             const int64_t x = (int64_t)xx - kPad;
-            uint32_t colA = 0, colB = 0;  // padding: zero scores
+            uint2 v = {0u, 0u};  // padding: zero scores
             if (x >= 0 && x < (int64_t)pd.text_len)
             {
-                const int tA = min(max((int)text[pd.text_off + x], 0), A - 1);
-                const int tB = min(max((int)text[pb.text_off + x], 0), A - 1);
-                for (int r = 0; r < A; ++r)
-                {
-                    colA |= ((uint32_t)table[r * A + tA] & 0xffu) << (8 * r);
-                    colB |= ((uint32_t)table[r * A + tB] & 0xffu) << (8 * r);
-                }
+                v.x = prof[min(max((int)text[pd.text_off + x], 0), A - 1)];
+                v.y = prof[min(max((int)text[pb.text_off + x], 0), A - 1)];
             }
-            codes[pd.code_off + 2 * xx] = (int32_t)colA;
-            codes[pd.code_off + 2 * xx + 1] = (int32_t)colB;
+            col[xx] = v;
         }
         return;
     }
@@ -861,7 +866,9 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         for (auto &d : pl->pairs) nmax = std::max<uint64_t>(nmax, std::max(d.text_len, d.pattern_len));
         // (text profiles: one thread per dword and alphabet row)
         const uint64_t work = pl->sk == kArr8 ? (nmax / 4 + kPad) * (uint64_t)pl->A : nmax;
-        const int gx = (int)std::min<uint64_t>((work + 255) / 256, 1024);
+        // at most ~8192 blocks in all: many small pairs loop inside their blocks rather than paying
+        // for block dispatch (4096 pairs x 8 blocks took 50 us, mostly dispatch)
+        const int gx = (int)std::min<uint64_t>((work + 255) / 256, std::max(1, std::min(1024, 8192 / np)));
         for (int y0 = 0; y0 < np; y0 += 65534)
         {
             // pairs beyond 65535 are handled by re-basing the pair pointer
