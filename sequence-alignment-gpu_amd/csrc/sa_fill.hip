@@ -290,7 +290,8 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
 }
 
 // Register state of the hand-scheduled steady steps (R = 1, kArr8; sa_fill_steps.inc, generated by
-// tools/gen_fill_asm.py): Q / Qn / diag rotate roles every step, F alternates with F2.
+// tools/gen_fill_asm.py): Q, Qn, diag and F rotate through the roles with period 4, so after a body
+// of U = 16 steps every value is back in its field (F2 is a spare).
 struct StepRegs {
     int Q, Qn, diag, F, F2;
     uint32_t acc0, acc1, acc2;
@@ -302,24 +303,6 @@ struct StepRegs {
     int ctag;             // HP: raw lap tag the feed entries must carry
     int msb;              // 0x80000000 in a VGPR (the bitop3 operand that applies raw tags)
     uint64_t bad;         // HP: lanes 0..U-1 whose feed entry did not carry it
-    template <int K>
-    __device__ __forceinline__ void rotate()
-    {
-        if constexpr (K == 1)
-        {
-            const int a = Q;
-            Q = Qn;
-            Qn = diag;
-            diag = a;
-        }
-        else if constexpr (K == 2)
-        {
-            const int a = Q;
-            Q = diag;
-            diag = Qn;
-            Qn = a;
-        }
-    }
 };
 template <bool LOCAL, bool HN, bool HP>
 __device__ __forceinline__ void steps_asm(StepRegs &r);

@@ -8,20 +8,23 @@ reads, and an s_nop costs an issue slot (4 cycles) like a VALU op. Scheduled by 
 step's two lane moves landed right behind their producers (one to two s_nops per step, plus a
 register copy for the bottom-row register), 13-15 issue slots per step; here every DPP sits at least
 two instructions behind its inputs with independent work in between, so a global step is exactly
-its 9 VALU ops (10 with a strip below) and nothing else.
+its 9 VALU ops and nothing else.
 
-One step (roles rotate A -> B -> C every step; F alternates between two registers):
-    b   Qn = A shifted down one lane (wave_shl:1); with HN its old value, preloaded, is the previous
-        step's bottom-row value F, which lane 63 keeps (sa_fill.hip run_body)
-    c   A = F shifted up one lane (wave_shr:1), in place: lane 0 keeps the feed value = `up`
+One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left, period 4):
+    b   Qn = Q shifted down one lane (wave_shl:1), written into the register of F two steps back
+        (dead); with HN its lane 63 keeps that step's bottom-row value F (sa_fill.hip run_body)
+    c   Q = F shifted up one lane (wave_shr:1), in place: lane 0 keeps the feed value = `up`
     d   D = diag + sext(score byte)          (SDWA byte select of the text-profile word)
     e   M = max(left, up)                    left = F of the previous step
     f   t1 = left - up                       -> plane 1 (raw up > left / raw TOP)
     g   global: F' = max(D, M) | local: X = max(D, M), F' = X -sat g, t2 = F' - 1 (STOP), key
+        (F' goes to the diag register, dead after d)
     h   t0 = M - D                           -> plane 0 (DIAG)
-    a'  (HN) C = F'                          preload of the next step's b (C held diag, now dead)
     i/j/k  push the sign bits into the plane words (v_alignbit acc, acc, t, 31)
-The next step uses Q = B (old Qn), Qn = C, diag = A (this step's up).
+A global step is its 9 VALU ops with or without a strip below: the queue's bottom-row values run
+one step later than the C++ bodies' (whose Qn takes F of the previous step through a register
+copy, 1 VALU per step), and the publish at the body's end shifts the queue once more with F of the
+step before last in lane 63, which gives the same 16 values (1 VALU per body instead of 16).
 
 Local keys: key' = (F' << kb) - q, its running maximum bm over the block (one v_max3 per two
 steps: keys alternate between two registers); the caller adds the body's key base
@@ -66,49 +69,47 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     if hn:
         k += 2
     MSB = f"%{k}"
-    roles = [A, B, C]
-    fregs = [FA, FB]
+    # four registers rotate through the roles with period 4 (U = 16 returns them to their operands):
+    # at step k, regs[k % 4] takes the shifted queue (Qn; it held F of step k-2, dead), regs[k-1] is
+    # Q (shifted down, then overwritten in place by up), regs[k-2] is diag (then takes F'), regs[k-3]
+    # is F of the previous step (left). Lane 63 of each Qn thus takes the bottom-row value of step
+    # k-2 instead of k-1; the publish restores the order with one more shift whose `old` is F of the
+    # step before last (lanes 64-U..63 = steps s0-1 .. s0+U-2, as the C++ bodies publish).
+    regs = [B, FA, C, A]  # at entry: regs[3] = Q, regs[1] = F (left), regs[2] = diag, regs[0] dead
     out = []
-    if hn:
-        out.append(f"v_mov_b32 {B}, {FA}")  # preload of the first step's Qn (the previous step's F)
-    out.append("s_nop 1")  # the compiler's last writes of Q / F / the preload stand right before
+    out.append("s_nop 1")  # the compiler's last writes of Q / F stand right before
     for k, q in enumerate(range(qb, qe)):
-        a, b, c = roles
+        qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
         if hp and q == PF_STEP:
             out.append(f"ds_read_b32 {PF}, {PFA}")
-        fp, fn = fregs[k % 2], fregs[(k + 1) % 2]
-        last = q == qe - 1
         if hn:
-            out.append(f"v_mov_b32_dpp {b}, {a} wave_shl:1 row_mask:0xf bank_mask:0xf")
+            out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf")
         else:
-            out.append(f"v_mov_b32_dpp {b}, {a} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-        out.append(f"v_mov_b32_dpp {a}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
-        out.append(f"v_add_u32_sdwa {D}, {c}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+            out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        out.append(f"v_mov_b32_dpp {qr}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
+        out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
                    f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
-        out.append(f"v_max_i32_e32 {M}, {fp}, {a}")
-        out.append(f"v_sub_u32_e32 {T1}, {fp}, {a}")
+        out.append(f"v_max_i32_e32 {M}, {fp}, {qr}")
+        out.append(f"v_sub_u32_e32 {T1}, {fp}, {qr}")
         if not local:
-            out.append(f"v_max_i32_e32 {fn}, {D}, {M}")
+            out.append(f"v_max_i32_e32 {dg}, {D}, {M}")
             out.append(f"v_sub_u32_e32 {T0}, {M}, {D}")
-            if hn and not last:
-                out.append(f"v_mov_b32_e32 {c}, {fn}")
             out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
             out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
         else:
             out.append(f"v_max_i32_e32 {X}, {D}, {M}")
             out.append(f"v_sub_u32_e32 {T0}, {M}, {D}")
-            out.append(f"v_sub_u32_e64 {fn}, {X}, {G} clamp")
+            out.append(f"v_sub_u32_e64 {dg}, {X}, {G} clamp")
             out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
-            out.append(f"v_add_u32_e32 {T2}, -1, {fn}")
+            out.append(f"v_add_u32_e32 {T2}, -1, {dg}")
             kreg = KEY if k % 2 == 0 else KEY2
-            out.append(f"v_lshl_add_u32 {kreg}, {fn}, {KB}, {-q}")
-            if hn and not last:
-                out.append(f"v_mov_b32_e32 {c}, {fn}")
+            out.append(f"v_lshl_add_u32 {kreg}, {dg}, {KB}, {-q}")
             out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
             if k % 2 == 1:
                 out.append(f"v_max3_i32 {BM}, {BM}, {KEY}, {KEY2}")
             out.append(f"v_alignbit_b32 {ACC2}, {ACC2}, {T2}, 31")
-        roles = [b, c, a]
+    nst = qe - qb
+    assert nst % 4 == 0, "the register rotation needs whole periods"
     if hp:
         out.append("s_waitcnt lgkmcnt(0)")  # the feed read (issued 4 steps ago) is there
         # tag check: x = entry ^ expected tag (the value when it matches; bitop3 0xD2 = a ^ (~b & c)),
@@ -118,24 +119,21 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
         out.append(f"v_cmp_gt_i32_e64 {BAD}, 0, {PF}")
         out.append(f"s_and_b64 {BAD}, {BAD}, 0xffff")
     if hn:
-        # publish: lanes 48..63 of the accumulated Q (now role B) with the body's lap tag; the write
-        # stays in flight past the block (the compiler sees no LDS operation it would wait for)
-        q_final = [A, B, C][U % 3]
-        out.append(f"v_bitop3_b32 {T0}, {q_final}, {PTAG}, {MSB} bitop3:0xf2")  # a | (~b & c)
+        # publish: the queue shifted once more into the register of F of the step before last (dead),
+        # whose lane 63 keeps that step's bottom-row value; lanes 64-U..63 with the body's lap tag. The
+        # write stays in flight past the block (the compiler sees no LDS operation it would wait for)
+        out.append(f"v_mov_b32_dpp {regs[0]}, {regs[3]} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        out.append(f"v_bitop3_b32 {T0}, {regs[0]}, {PTAG}, {MSB} bitop3:0xf2")  # a | (~b & c)
         out.append(f"ds_write_b32 {PADDR}, {T0}")
     return "\\n\\t".join(out)
-
-
-def rot(n):
-    return n % 3
 
 
 def main():
     lines = [
         "// GENERATED by tools/gen_fill_asm.py -- do not edit. Hand-scheduled steady steps of the R = 1",
         "// kArr8 fill (see the generator's docstring for the schedule and its hazard rules).",
-        "// steps_asm<LOCAL, HN, HP>(r): the U = 16 steps of a body; Q / Qn / diag rotate by one role per",
-        "// step, F alternates between two registers; with HP the next body's feed read (address",
+        "// steps_asm<LOCAL, HN, HP>(r): the U = 16 steps of a body; Q / Qn / diag / F rotate through the",
+        "// roles with period 4 (back in place after the body); with HP the next body's feed read (address",
         "// r.pfaddr) is issued after step 12 and waited for at the end (result r.pf).",
         "#pragma once",
         "",
@@ -168,7 +166,6 @@ def main():
                     ins += ", \"v\"(r.msb)"
                 lines.append(f"        : {ins}" + (" : \"scc\");" if hp else ");"))
                 lines.append("    (void)D; (void)M; (void)t0; (void)t1; (void)X; (void)t2; (void)key; (void)key2;")
-                lines.append(f"    r.rotate<{rot(U)}>();")
                 lines.append("}")
                 lines.append("")
     open(OUT, "w").write("\n".join(lines))
