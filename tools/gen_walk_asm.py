@@ -52,12 +52,14 @@ def gen(local: bool) -> list[str]:
         if k > 0:
             # the next row's word, under the search's latency
             e(f"v_readlane_b32 {nw}, %[w0], {k - 1}")
-        if local:
-            e(f"s_xor_b32 s86, {p}, 1")
-            e("s_bitcmp1_b32 s92, s86")
-            e(f"s_cbranch_scc1 .Lstop{k}_%=")
         e(f"s_bitcmp1_b32 {p}, 0")
         e(f"s_addc_u32 %[u], %[u], {p}")
+        if local:
+            # STOP test after the position update (off the row chain; the stub undoes the update:
+            # p is even for a STOP)
+            e(f"s_xor_b32 s86, {p}, 1")
+            e("s_bitcmp1_b32 s92, s86")
+            e(f"s_cbranch_scc1 .Lstopm{k}_%=")
     e(f"v_writelane_b32 %[rec], {prec(0)}, 0")
     e("s_mov_b32 %[st], -1")
     e(f"s_mov_b32 %[lp], {prec(0)}")
@@ -107,6 +109,8 @@ def gen(local: bool) -> list[str]:
         e(f"s_mov_b32 %[st], {k}")
         e("s_branch .Lout_%=")
         if local:
+            e(f".Lstopm{k}_%=:")
+            e(f"s_sub_u32 %[u], %[u], {p}")
             e(f".Lstop{k}_%=:")
             e(f"s_mov_b32 %[st], {0x100 | k}")
             e(f"s_mov_b32 %[lp], {p}")
