@@ -128,6 +128,12 @@ def main():
         segc = np.diff(mt[:, ok], axis=1) / 4096.0
         rec["clk_per_step_by_segment_every32"] = [[k] + [round(float(x), 1) for x in segc[k]] for k in range(0, len(segc), 32)]
         rec["checkpoint_us"] = [[k] + [round(float(x - t0) * 0.01, 1) for x in prog[k, ok]] for k in range(0, len(seg), 64)]
+        # slow-path counters per strip: feed checks that failed / their re-reads, publishes that
+        # waited for the consumer / their polls (bodies per strip = nsteps / 16)
+        sc = tl[:, 36:40].astype(np.int64)
+        rec["slow_paths_mean_per_strip"] = {nm: round(float(sc[1:, i].mean()), 1) for i, nm in
+                                            enumerate(("feed_slow", "feed_spins", "pub_slow", "pub_spins"))}
+        rec["feed_slow_by_wave_in_group"] = [round(float(sc[w::W, 0].mean()), 1) for w in range(W)]
     print(json.dumps(rec))
     b.close()
 
