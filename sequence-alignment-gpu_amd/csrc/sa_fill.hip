@@ -416,6 +416,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     int consKnown = 0;   // columns the consumer of rout is known to have read
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
     uint32_t dbgFeedSlow = 0, dbgFeedSpins = 0, dbgPubSlow = 0, dbgPubSpins = 0;  // slow-path counts
+    uint32_t dbgFeedSlowSteady = 0, dbgFeedSpinsSteady = 0;  // the same past column 4096
 #endif
     // Feed values for the body starting at step base (columns base+1 .. base+U, lanes 0..U-1 of Q)
     // are read kPfLead steps before that body starts, in the middle of the previous body: early
@@ -485,11 +486,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
                 uint64_t t0 = 0;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
                 ++dbgFeedSlow;
+                if (base >= 4096) ++dbgFeedSlowSteady;
 #endif
                 for (uint32_t spin = 1;; ++spin)
                 {
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
                     ++dbgFeedSpins;
+                    if (base >= 4096) ++dbgFeedSpinsSteady;
 #endif
                     if (spin > 16) __builtin_amdgcn_s_sleep(1);
                     x = ds_read_sync(feed_addr(base)) ^ tag;
@@ -737,6 +740,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         tl[37] = dbgFeedSpins;
         tl[38] = dbgPubSlow;
         tl[39] = dbgPubSpins;
+        tl[40] = dbgFeedSlowSteady;
+        tl[41] = dbgFeedSpinsSteady;
 #endif
         tl[5] = __builtin_amdgcn_s_memtime();
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)

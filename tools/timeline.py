@@ -100,6 +100,10 @@ def main():
         "cus_used": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
         "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
         "simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in hw[:8]],
+        # pace by the strip's wave slot in its group and by its SIMD (does the wave that shares its
+        # SIMD with the group's I/O wave run slower?)
+        "ns_per_step_by_wave_in_group": [round(float(step_ns[w::W].mean()), 2) for w in range(W)],
+        "ns_per_step_by_simd": [round(float(step_ns[((hw >> 4) & 3) == q].mean()), 2) if (((hw >> 4) & 3) == q).any() else None for q in range(4)],
     }
     prog = tl[:, 6:16].astype(np.int64)
     iop = tl[:, 16:26].astype(np.int64)
@@ -130,9 +134,10 @@ def main():
         rec["checkpoint_us"] = [[k] + [round(float(x - t0) * 0.01, 1) for x in prog[k, ok]] for k in range(0, len(seg), 64)]
         # slow-path counters per strip: feed checks that failed / their re-reads, publishes that
         # waited for the consumer / their polls (bodies per strip = nsteps / 16)
-        sc = tl[:, 36:40].astype(np.int64)
+        sc = tl[:, 36:42].astype(np.int64)
         rec["slow_paths_mean_per_strip"] = {nm: round(float(sc[1:, i].mean()), 1) for i, nm in
-                                            enumerate(("feed_slow", "feed_spins", "pub_slow", "pub_spins"))}
+                                            enumerate(("feed_slow", "feed_spins", "pub_slow", "pub_spins",
+                                                       "feed_slow_past_4096", "feed_spins_past_4096"))}
         rec["feed_slow_by_wave_in_group"] = [round(float(sc[w::W, 0].mean()), 1) for w in range(W)]
     print(json.dumps(rec))
     b.close()
