@@ -594,9 +594,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
     const int A = P->alphabet_size;
     if (A < 1 || A > 32) return fail(SA_ERR_INVALID, "alphabet_size must be 1..32");
     if (P->mode != SA_GLOBAL && P->mode != SA_LOCAL) return fail(SA_ERR_INVALID, "mode must be SA_GLOBAL or SA_LOCAL");
-    // the reference takes a positive gap penalty (utilities.cpp parseArguments); the local
-    // recurrence's saturating subtraction relies on g >= 0
-    if (P->gap_penalty < 0) return fail(SA_ERR_UNSUPPORTED, "gap_penalty must be >= 0");
+    // any int gap penalty, as the reference's CLI (std::stoi, utilities.cpp:188-199) and its fill
+    // (alignSequenceCPU.cpp:175-176, 259-260) take it; the range bound below rejects what int32 cannot hold
     const int64_t g = P->gap_penalty;
     int64_t smax = INT32_MIN, smin = INT32_MAX, sabs = 0;
     for (int e = 0; e < A * A; ++e)
@@ -707,7 +706,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         // pair-packed fill (fill_pair_kernel): global, lone strips of one shape, DNA-sized alphabet,
         // every S + 2g in [0, 255] and every value within u16 (see process_pair)
         bool pair = P->mode == SA_GLOBAL && !pl->chain && np >= 2 && np % 2 == 0 && A <= 4 && R >= 16 &&
-                    !knobs().no_pair16;
+                    g > 0 && !knobs().no_pair16;
         int64_t smaxp = 0;
         for (int e = 0; e < A * A; ++e)
         {

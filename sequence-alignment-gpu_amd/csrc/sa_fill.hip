@@ -173,14 +173,16 @@ struct Codes {
 //            s < k. Forcing the substitution score of those virtual cells to 0 keeps their state at
 //            the boundary value (see the recurrences), so lane k enters column 1 with exactly the
 //            column-0 state. Text profiles need no kStart bodies: their padding scores are 0.
-//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row, and
-//            local strips' last bodies).
+//            Local with g < 0 cannot use this (an all-zero neighbourhood gives H = -g, not 0): its
+//            first bodies are kGeneric instead.
+//   kGeneric lanes outside [1, n] keep their state (the strip holding the global score's row,
+//            local strips' last bodies, and local strips' first bodies when g < 0).
 enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // Recurrences (per lane-row; diag/up/left are the neighbours' values):
 //   global, shifted domain F = H + g(i+j): F = max(Fdiag + S + 2g, Fleft, Fup), boundaries 0;
 //     DIAG iff Fdiag + S + 2g > max(Fleft, Fup); plane 1 = raw "up > left".
-//   local, H with the gap folded into the score: X = max(Hdiag + S + g, max(Hleft, Hup)),
-//     H = max(X - g, 0) (one saturating subtraction: X >= 0); DIAG iff Hdiag + S + g > max(Hleft,
+//   local, H with the gap folded into the score: X = max(Hdiag + S + g, max(Hleft, Hup), g),
+//     H = X - g (= max(X' - g, 0) for g > 0, X' - g for g <= 0: X' >= 0); DIAG iff Hdiag + S + g > max(Hleft,
 //     Hup) (the reference's D > max(L, U) with every candidate shifted by +g); raw TOP iff Hup >
 //     Hleft; STOP iff H == 0 (alignSequenceCPU.cpp:175-190).
 // Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
@@ -241,8 +243,9 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
             }
             else
             {
-                const unsigned X = (unsigned)max(D, M);
-                Fn = (int)__builtin_elementwise_sub_sat(X, (unsigned)g);
+                // H = max(X, g) - g: max(X - g, 0) for g > 0, and X - g for g <= 0 (X >= 0)
+                const int X = max(max(D, M), g);
+                Fn = X - g;
                 acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
                 const int key = (Fn << kb) + Ks;
                 if constexpr (RAMP) best[rho] = act ? max(best[rho], key) : best[rho];
@@ -704,14 +707,21 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         // steady bodies whose next feed lies in columns 1..n (base + U <= n: every lane is needed and
         // delivered, by a neighbour wave or by the I/O wave, which copies columns 1..n), then the rest
         // of the steady bodies with a lane count
-        if constexpr (!kIsArr<SK>) phase(KStart{}, std::false_type{}, min(kWave, sTail));
+        if (LOCAL && g < 0) phase(KGeneric{}, std::false_type{}, min(kWave, sTail));
+        else if constexpr (!kIsArr<SK>) phase(KStart{}, std::false_type{}, min(kWave, sTail));
         phase(KSteady{}, std::true_type{}, min(sTail, max(0, (n - U) / (2 * U) * (2 * U))));
         phase(KSteady{}, std::false_type{}, sTail);
         phase(KGeneric{}, std::false_type{}, nSteps);
     }
     else
     {
-        if constexpr (!kIsArr<SK>)
+        if (LOCAL && g < 0)
+            for (; s0 < min(kWave, sTail); s0 += 2 * U)
+            {
+                body(KGeneric{}, P0{}, std::false_type{}, s0, TA, TB);
+                body(KGeneric{}, P1{}, std::false_type{}, s0 + U, TB, TA);
+            }
+        else if constexpr (!kIsArr<SK>)
             for (; s0 < min(kWave, sTail); s0 += 2 * U)
             {
                 body(KStart{}, P0{}, std::false_type{}, s0, TA, TB);

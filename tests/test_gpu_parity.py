@@ -74,6 +74,33 @@ def test_random_pairs(eng, golden, rows_per_lane):
         assert same_result(got, case["result"]), (k, case["tag"], len(t), len(p))
 
 
+@pytest.mark.parametrize("rows_per_lane", [0, 1, 2, 4, 8, 16, 32])
+def test_gap_pairs(eng, rows_per_lane):
+    """Gap penalties 0, -1, -2, -5, both modes, DNA and protein, single strips and multi-group chains
+    (tests/golden/gap_pairs.json, from the reference: its CLI takes any int, utilities.cpp:188-199)."""
+    from conftest import load
+    for k, case in enumerate(load("gap_pairs.json")):
+        t, p, S = _inputs(case)
+        got = eng.align_pair(case["mode"], t, p, S, case["gap"], rows_per_lane=rows_per_lane)
+        assert same_result(got, case["result"]), (k, case["tag"], case["gap"], len(t), len(p))
+
+
+def test_gap_pairs_batched(eng):
+    """The same cases as one plan per (mode, alphabet, gap, matrix): many pairs per fill launch."""
+    from conftest import load
+    from sa_amd.batch import DeviceBatch
+    key = lambda c: (c["mode"], c["A"], c["gap"], c["matrix"])
+    for (mode, A, gap, mat), grp in itertools.groupby(sorted(load("gap_pairs.json"), key=key), key=key):
+        grp = list(grp)
+        b = DeviceBatch(mode, matrix(mat, A), gap, [encode(c["text"], A) for c in grp],
+                        [encode(c["pattern"], A) for c in grp])
+        res = b.run()
+        for k, c in enumerate(grp):
+            at, ap = b.alignment(k)
+            assert same_result(dict(res[k], aligned_text=at, aligned_pattern=ap), c["result"]), (c["tag"], gap, mode)
+        b.close()
+
+
 @pytest.mark.parametrize("rows_per_lane", [1, 2, 4, 32])
 def test_seeded_vs_oracle(eng, rows_per_lane):
     """Multi-strip hand-offs (pattern >> 64*R rows) on seeded DNA and protein pairs."""
@@ -168,9 +195,10 @@ def test_batch_plan_config5(eng, golden):
     b.close()
 
 
+@pytest.mark.parametrize("gap", [5, 0, -3])
 @pytest.mark.parametrize("rows_per_lane", [1, 2, 4, 8, 16, 32])
 @pytest.mark.parametrize("mode", [0, 1])
-def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane):
+def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane, gap):
     """The fill alone, cell by cell: the engine's DIRECTION matrix (decoded from its bit-planes) equals
     the reference's (m+1)x(n+1) byte matrix M (alignSequenceCPU.cpp:116-284) on every cell."""
     from sa_amd.batch import DeviceBatch
@@ -178,11 +206,11 @@ def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane):
     for k, (n, m) in enumerate([(1500, 1400), (700, 700), (130, 66)]):
         t = synthetic.random_sequence(500 + k, n, 4)
         p = synthetic.mutate(t, 600 + k, 4, m)
-        b = DeviceBatch(mode, S, 5, [t], [p], rows_per_lane=rows_per_lane)
+        b = DeviceBatch(mode, S, gap, [t], [p], rows_per_lane=rows_per_lane)
         b.fill()
         got = b.directions(0)
         exp = np.empty((m + 1) * (n + 1), np.uint8)
-        oracle.fill_only(mode, t, p, S, 5, exp)
+        oracle.fill_only(mode, t, p, S, gap, exp)
         bad = int((got != exp).sum())
         b.close()
         assert bad == 0, (n, m, bad)

@@ -43,6 +43,13 @@ def test_random_pairs(golden):
         assert same_result(_run(case), case["result"]), (k, case["tag"])
 
 
+def test_gap_pairs():
+    """Gap penalties 0, -1, -2, -5 (tests/golden/make_gaps.py, from the reference)."""
+    from conftest import load
+    for k, case in enumerate(load("gap_pairs.json")):
+        assert same_result(_run(case), case["result"]), (k, case["tag"], case["gap"])
+
+
 @pytest.mark.parametrize("name", ["cfg2_dna_global_8192_uniform", "cfg2_dna_global_8192_mutated",
                                   "cfg4_protein_global_4096_blosum50", "cfg4_protein_local_4096_blosum50",
                                   "cfg5_batch_pair_0"])
@@ -69,6 +76,6 @@ def test_oracle_matches_reference_binary_on_fresh_inputs():
         m = int(rng.integers(1, n + 1))
         t = rng.integers(0, 4, n).astype(np.int8)
         p = synthetic.mutate(t, k, 4, m) if k % 2 else rng.integers(0, 4, m).astype(np.int8)
-        jobs.append((k % 2, t, p, S, int(rng.integers(1, 12))))
+        jobs.append((k % 2, t, p, S, int(rng.integers(-6, 12))))
     for job, r in zip(jobs, oracle.ref_align_batch(jobs)):
         assert oracle.align(*job) == r

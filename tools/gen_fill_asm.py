@@ -17,7 +17,7 @@ One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left,
     d   D = diag + sext(score byte)          (SDWA byte select of the text-profile word)
     e   M = max(left, up)                    left = F of the previous step
     f   t1 = left - up                       -> plane 1 (raw up > left / raw TOP)
-    g   global: F' = max(D, M) | local: X = max(D, M), F' = X -sat g, t2 = F' - 1 (STOP), key
+    g   global: F' = max(D, M) | local: X = max(D, M, g), F' = X - g, t2 = F' - 1 (STOP), key
         (F' goes to the diag register, dead after d)
     h   t0 = M - D                           -> plane 0 (DIAG)
     i/j/k  push the sign bits into the plane words (v_alignbit acc, acc, t, 31)
@@ -97,9 +97,10 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
             out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
             out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
         else:
-            out.append(f"v_max_i32_e32 {X}, {D}, {M}")
+            # H = max(X, g) - g = max(X - g, 0) for g > 0 and X - g (never 0 clamped) for g <= 0
+            out.append(f"v_max3_i32 {X}, {D}, {M}, {G}")
             out.append(f"v_sub_u32_e32 {T0}, {M}, {D}")
-            out.append(f"v_sub_u32_e64 {dg}, {X}, {G} clamp")
+            out.append(f"v_subrev_u32_e32 {dg}, {G}, {X}")
             out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
             out.append(f"v_add_u32_e32 {T2}, -1, {dg}")
             kreg = KEY if k % 2 == 0 else KEY2
