@@ -98,8 +98,8 @@ typedef struct sa_host_pair {
 } sa_host_pair;
 
 /* Align num_pairs independent pairs with one scoring scheme over devices 0..num_gpus-1 of this
- * process (one host thread and one plan per device; results gathered to device 0 with RCCL).
- * Synchronous. results: num_pairs entries. aligned_text / aligned_pattern: NULL (scores only) or
+ * process (one host thread and one plan per device; the per-pair results are gathered to device 0
+ * with RCCL, loaded on first use, communicators kept for the process). Synchronous. results: num_pairs entries. aligned_text / aligned_pattern: NULL (scores only) or
  * num_pairs host buffers, buffer i of at least text_len + pattern_len bytes, receiving pair i's
  * num_alignment_bytes letters in forward order. The pair -> device deal is sa_batch_deal's. If
  * num_gpus exceeds the device count, devices are shared round-robin (no RCCL then). */
@@ -110,6 +110,12 @@ int sa_align_batch(const sa_params *params, const sa_host_pair *pairs, int64_t n
  * work cells[i] = text_len * pattern_len. Equal work: round-robin (i mod num_shards); otherwise
  * longest-processing-time (largest first to the least-loaded shard, ties to the lower shard). */
 int sa_batch_deal(const uint64_t *cells, int64_t num_pairs, int num_shards, int32_t *shard_of);
+
+/* Debug record of the calling thread's last sa_align_batch: shards used, whether the results came
+ * through the RCCL gather (1) or straight from each shard (0, shards sharing a device), each shard's
+ * wall time from upload to the end of its traceback (shard_ms: up to cap entries) and the gather's
+ * wall time (0 without RCCL). */
+int sa_batch_last_stats(int32_t *num_shards, int32_t *used_rccl, double *shard_ms, int32_t cap, double *gather_ms);
 
 /* ---- plans: many pairs, device-resident inputs, explicit stream ------------------------- */
 
@@ -142,7 +148,8 @@ uint64_t sa_plan_output_bytes(const sa_plan *plan);
  * pass (what a batch caller needs: one copy each instead of one per pair). text_buf / pattern_buf
  * hold buf_bytes >= sa_plan_output_bytes(plan) bytes; pair i's aligned text / pattern are the
  * results[i].num_alignment_bytes letters at text_buf + offsets[i] / pattern_buf + offsets[i]
- * (offsets: num_pairs entries). Returns SA_ERR_TIMEOUT if the fill aborted. */
+ * (offsets: num_pairs entries). results, text_buf and pattern_buf may each be NULL (not copied).
+ * Returns SA_ERR_TIMEOUT if the fill aborted. */
 int sa_plan_fetch_all(sa_plan *plan, sa_result *results, char *text_buf, char *pattern_buf, uint64_t buf_bytes,
                       uint64_t *offsets, void *stream);
 
@@ -162,6 +169,9 @@ const void *sa_plan_device_results(const sa_plan *plan);
 int sa_device_count(int *count);
 const char *sa_last_error(void);
 int sa_abi_version(void);
+/* Hash of the sources the library was built from (sequence-alignment-gpu_amd/python/sa_amd/buildid.py):
+ * callers compare it with the hash of the sources they ship with and refuse a stale binary. */
+const char *sa_build_id(void);
 /* Runs the engine's wave-level primitive self-test on `device` (DPP lane shifts, ballots);
  * returns SA_OK when the hardware behaves as the kernels assume. */
 int sa_selftest(int device);

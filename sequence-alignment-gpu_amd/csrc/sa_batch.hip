@@ -8,17 +8,24 @@
 //     (largest n*m first, to the least-loaded shard, ties to the lower shard), so shards finish
 //     together;
 //   * one host thread per shard: pack the shard's inputs into one text and one pattern arena,
-//     upload, one plan (sa_plan_*: one fill launch + one traceback launch for all its pairs), and
-//     copy its aligned-string arenas back into the caller's per-pair buffers;
+//     upload, one plan (sa_plan_*: one fill launch + one traceback launch for all its pairs), its
+//     sa_result array into a fixed-width RCCL send buffer, its aligned-string arenas to the host;
 //   * the exchange step: every shard's sa_result array is gathered to device 0 with RCCL
-//     (ncclGather over xGMI, one communicator per device from ncclCommInitAll) and copied to the
-//     caller's results from there. Shards that share a device (num_gpus > device count, a test
-//     mode for one-GPU machines) skip RCCL and copy their results directly.
+//     (ncclGather over xGMI) and the caller's results come from that gathered buffer only; the
+//     strings are copied into the caller's buffers after it, with the gathered lengths. RCCL is
+//     loaded on first use (dlopen: callers that never shard over several devices do not need it)
+//     and the communicators of a device set are created once per process. Shards that share a
+//     device (num_gpus > device count, a test mode for one-GPU machines) skip RCCL and take their
+//     results from their own plan.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -34,19 +41,71 @@ namespace {
 
 int fail_b(int code, const std::string &msg) { return sa::set_error(code, msg); }
 
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) { return std::chrono::duration<double, std::milli>(Clock::now() - t0).count(); }
+
+// ---- RCCL, loaded on first use -------------------------------------------------------------------
+struct Rccl {
+    bool tried = false, ok = false;
+    std::string err;
+    ncclResult_t (*commInitAll)(ncclComm_t *, int, const int *) = nullptr;
+    ncclResult_t (*groupStart)() = nullptr;
+    ncclResult_t (*groupEnd)() = nullptr;
+    ncclResult_t (*gather)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+};
+
+std::mutex g_batch_mu;  // one sa_align_batch at a time per process (shared communicators)
+
+Rccl &rccl()
+{
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h)
+    {
+        const char *e = dlerror();
+        r.err = std::string("cannot load librccl: ") + (e ? e : "?");
+        return r;
+    }
+    r.commInitAll = reinterpret_cast<decltype(r.commInitAll)>(dlsym(h, "ncclCommInitAll"));
+    r.groupStart = reinterpret_cast<decltype(r.groupStart)>(dlsym(h, "ncclGroupStart"));
+    r.groupEnd = reinterpret_cast<decltype(r.groupEnd)>(dlsym(h, "ncclGroupEnd"));
+    r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(h, "ncclGather"));
+    r.ok = r.commInitAll && r.groupStart && r.groupEnd && r.gather;
+    if (!r.ok) r.err = "librccl lacks ncclCommInitAll / ncclGroupStart / ncclGroupEnd / ncclGather";
+    return r;
+}
+
+// Communicators of devices 0..G-1, created once per process (never destroyed: RCCL tears them down
+// at exit; destroying them from a static destructor can run after the HIP runtime is gone).
+std::map<int, std::vector<ncclComm_t>> g_comms;
+
+// ---- shards -------------------------------------------------------------------------------------
 struct Shard {
     std::vector<int64_t> idx;  // global pair indices, in ascending order
     int device = 0;
     int rc = SA_OK;
     std::string err;
-    std::vector<sa_result> res;
-    sa_result *d_send = nullptr;  // RCCL send buffer (width entries)
+    std::vector<sa_result> res;    // own results (no RCCL only)
+    std::vector<char> ot, op;      // aligned-string arenas on the host
+    std::vector<uint64_t> off;     // each pair's offset in the arenas
+    sa_result *d_send = nullptr;   // RCCL send buffer (width entries), device `device`
+    hipStream_t st = nullptr;
+    double ms = 0;
 };
 
-// Runs one shard on its device: upload, plan, fill, traceback, strings back to the caller.
-void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, char *const *at, char *const *ap,
-               size_t width, bool rccl)
+thread_local int32_t t_last_shards = 0, t_last_rccl = 0;
+thread_local std::vector<double> t_last_ms;
+thread_local double t_last_gather_ms = 0;
+
+// Runs one shard on its device: upload, plan, fill, traceback; results into the RCCL send buffer
+// (rccl) or to the host, aligned-string arenas to the host (when the caller wants strings).
+void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, bool strings, size_t width, bool rccl_path)
 {
+    const Clock::time_point t0 = Clock::now();
     auto bad = [&](int code, const std::string &msg) {
         sh.rc = code;
         sh.err = msg;
@@ -69,57 +128,49 @@ void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, char *c
         if (h.text_len) std::memcpy(&ht[pp[q].text_offset], h.text, h.text_len);
         if (h.pattern_len) std::memcpy(&hpat[pp[q].pattern_offset], h.pattern, h.pattern_len);
     }
-    hipStream_t st = nullptr;
     char *dt = nullptr, *dp = nullptr;
     sa_plan *plan = nullptr;
     auto cleanup = [&]() {
         if (plan) sa_plan_destroy(plan);
         if (dt) (void)hipFree(dt);
         if (dp) (void)hipFree(dp);
-        if (st) (void)hipStreamDestroy(st);
     };
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&dt, ht.size()) != hipSuccess || hipMalloc((void **)&dp, hpat.size()) != hipSuccess)
+    if (hipMalloc((void **)&dt, ht.size()) != hipSuccess || hipMalloc((void **)&dp, hpat.size()) != hipSuccess)
     {
         (void)hipGetLastError();
         cleanup();
         return bad(SA_ERR_NOMEM, "sa_align_batch: device allocation failed");
     }
     int rc = SA_OK;
-    if (hipMemcpyAsync(dt, ht.data(), ht.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(dp, hpat.data(), hpat.size(), hipMemcpyHostToDevice, st) != hipSuccess)
+    if (hipMemcpyAsync(dt, ht.data(), ht.size(), hipMemcpyHostToDevice, sh.st) != hipSuccess ||
+        hipMemcpyAsync(dp, hpat.data(), hpat.size(), hipMemcpyHostToDevice, sh.st) != hipSuccess)
         rc = SA_ERR_HIP;
     if (!rc) rc = sa_plan_create(P, pp.data(), (int64_t)k, sh.device, &plan);
-    if (!rc) rc = sa_plan_fill(plan, dt, dp, st);
-    if (!rc) rc = sa_plan_traceback(plan, st);
-    if (!rc && rccl)
+    if (!rc) rc = sa_plan_fill(plan, dt, dp, sh.st);
+    if (!rc) rc = sa_plan_traceback(plan, sh.st);
+    if (!rc && rccl_path)
     {
         // the shard's results into the fixed-width RCCL send buffer (unused entries stay zero)
-        if (hipMemsetAsync(sh.d_send, 0, width * sizeof(sa_result), st) != hipSuccess ||
+        if (hipMemsetAsync(sh.d_send, 0, width * sizeof(sa_result), sh.st) != hipSuccess ||
             (k && hipMemcpyAsync(sh.d_send, sa_plan_device_results(plan), k * sizeof(sa_result),
-                                 hipMemcpyDeviceToDevice, st) != hipSuccess))
+                                 hipMemcpyDeviceToDevice, sh.st) != hipSuccess))
             rc = SA_ERR_HIP;
     }
     if (!rc)
     {
         const uint64_t nb = sa_plan_output_bytes(plan);
-        const bool strings = at || ap;
-        std::vector<char> ot(strings ? nb : 0), op(strings ? nb : 0);
-        std::vector<uint64_t> off(std::max<size_t>(1, k));
-        sh.res.resize(std::max<size_t>(1, k));
-        rc = sa_plan_fetch_all(plan, sh.res.data(), strings ? ot.data() : nullptr, strings ? op.data() : nullptr,
-                               nb, off.data(), st);
-        sh.res.resize(k);
-        for (size_t q = 0; !rc && strings && q < k; ++q)
-        {
-            const int64_t i = sh.idx[q];
-            const uint64_t L = sh.res[q].num_alignment_bytes;
-            if (at && at[i] && L) std::memcpy(at[i], &ot[off[q]], L);
-            if (ap && ap[i] && L) std::memcpy(ap[i], &op[off[q]], L);
-        }
+        sh.ot.assign(strings ? nb : 0, 0);
+        sh.op.assign(strings ? nb : 0, 0);
+        sh.off.assign(std::max<size_t>(1, k), 0);
+        if (!rccl_path) sh.res.resize(std::max<size_t>(1, k));
+        // (also synchronises the stream: the send buffer is complete before the gather)
+        rc = sa_plan_fetch_all(plan, rccl_path ? nullptr : sh.res.data(), strings ? sh.ot.data() : nullptr,
+                               strings ? sh.op.data() : nullptr, nb, sh.off.data(), sh.st);
+        if (!rccl_path) sh.res.resize(k);
     }
     if (rc) bad(rc, sa_last_error());
     cleanup();
+    sh.ms = ms_since(t0);
 }
 
 }  // namespace
@@ -150,6 +201,15 @@ int sa_batch_deal(const uint64_t *cells, int64_t num_pairs, int num_shards, int3
     return SA_OK;
 }
 
+int sa_batch_last_stats(int32_t *num_shards, int32_t *used_rccl, double *shard_ms, int32_t cap, double *gather_ms)
+{
+    if (num_shards) *num_shards = t_last_shards;
+    if (used_rccl) *used_rccl = t_last_rccl;
+    for (int32_t s = 0; shard_ms && s < cap && s < (int32_t)t_last_ms.size(); ++s) shard_ms[s] = t_last_ms[s];
+    if (gather_ms) *gather_ms = t_last_gather_ms;
+    return SA_OK;
+}
+
 int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pairs, int num_gpus,
                    sa_result *results, char *const *aligned_text, char *const *aligned_pattern)
 {
@@ -165,6 +225,7 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         for (uint64_t x = 0; x < h.pattern_len; ++x)
             if (h.pattern[x] < 0 || h.pattern[x] >= P->alphabet_size) return fail_b(SA_ERR_INVALID, "pattern byte outside the alphabet");
     }
+    std::lock_guard<std::mutex> lock(g_batch_mu);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return fail_b(SA_ERR_HIP, "no HIP device");
     int cur = 0;
@@ -182,18 +243,20 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         sh[s].device = s % ndev;
         width = std::max(width, sh[s].idx.size());
     }
+    t_last_shards = G;
+    t_last_rccl = 0;
+    t_last_ms.assign(G, 0.0);
+    t_last_gather_ms = 0;
     // RCCL only across distinct devices (one communicator per device)
-    const bool rccl = G > 1 && G <= ndev;
-    std::vector<ncclComm_t> comms;
+    const bool use_rccl = G > 1 && G <= ndev;
     sa_result *d_gather = nullptr;
     auto release = [&]() {
-        for (ncclComm_t c : comms) (void)ncclCommDestroy(c);
         for (Shard &x : sh)
-            if (x.d_send)
-            {
-                (void)hipSetDevice(x.device);
-                (void)hipFree(x.d_send);
-            }
+        {
+            (void)hipSetDevice(x.device);
+            if (x.d_send) (void)hipFree(x.d_send);
+            if (x.st) (void)hipStreamDestroy(x.st);
+        }
         if (d_gather)
         {
             (void)hipSetDevice(0);
@@ -201,17 +264,39 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         }
         (void)hipSetDevice(cur);
     };
-    if (rccl)
+    for (Shard &x : sh)
     {
-        std::vector<int> devs(G);
-        for (int s = 0; s < G; ++s) devs[s] = s;
-        comms.resize(G);
-        if (ncclCommInitAll(comms.data(), G, devs.data()) != ncclSuccess)
+        (void)hipSetDevice(x.device);
+        if (hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking) != hipSuccess)
         {
-            comms.clear();
+            (void)hipGetLastError();
             release();
-            return fail_b(SA_ERR_HIP, "sa_align_batch: ncclCommInitAll failed");
+            return fail_b(SA_ERR_HIP, "sa_align_batch: stream creation failed");
         }
+    }
+    std::vector<ncclComm_t> *comms = nullptr;
+    if (use_rccl)
+    {
+        Rccl &R = rccl();
+        if (!R.ok)
+        {
+            release();
+            return fail_b(SA_ERR_HIP, "sa_align_batch: " + R.err);
+        }
+        auto it = g_comms.find(G);
+        if (it == g_comms.end())
+        {
+            std::vector<int> devs(G);
+            std::iota(devs.begin(), devs.end(), 0);
+            std::vector<ncclComm_t> c(G);
+            if (R.commInitAll(c.data(), G, devs.data()) != ncclSuccess)
+            {
+                release();
+                return fail_b(SA_ERR_HIP, "sa_align_batch: ncclCommInitAll failed");
+            }
+            it = g_comms.emplace(G, std::move(c)).first;
+        }
+        comms = &it->second;
         for (int s = 0; s < G; ++s)
         {
             (void)hipSetDevice(s);
@@ -230,61 +315,60 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
             return fail_b(SA_ERR_NOMEM, "sa_align_batch: RCCL buffer allocation failed");
         }
     }
+    const bool strings = aligned_text || aligned_pattern;
     std::vector<std::thread> th;
     for (int s = 0; s < G; ++s)
-        th.emplace_back(run_shard, P, pairs, std::ref(sh[s]), aligned_text, aligned_pattern, width, rccl);
+        th.emplace_back(run_shard, P, pairs, std::ref(sh[s]), strings, width, use_rccl);
     for (std::thread &t : th) t.join();
+    for (int s = 0; s < G; ++s) t_last_ms[s] = sh[s].ms;
     for (const Shard &x : sh)
         if (x.rc)
         {
             release();
             return fail_b(x.rc, "sa_align_batch: shard on device " + std::to_string(x.device) + ": " + x.err);
         }
-    if (rccl)
+    // per-pair results: gathered over RCCL (the exchange step) or straight from each shard
+    std::vector<sa_result> all;
+    if (use_rccl)
     {
-        // the path's exchange step: every shard's results to device 0 (ncclGather, xGMI), one group
-        std::vector<hipStream_t> streams(G, nullptr);
-        bool ok = true;
+        const Clock::time_point tg = Clock::now();
+        Rccl &R = rccl();
+        bool ok = R.groupStart() == ncclSuccess;
         for (int s = 0; s < G && ok; ++s)
-        {
-            (void)hipSetDevice(s);
-            ok = hipStreamCreateWithFlags(&streams[s], hipStreamNonBlocking) == hipSuccess;
-        }
-        ok = ok && ncclGroupStart() == ncclSuccess;
-        for (int s = 0; s < G && ok; ++s)
-            ok = ncclGather(sh[s].d_send, s == 0 ? d_gather : nullptr, width * sizeof(sa_result), ncclUint8, 0,
-                            comms[s], streams[s]) == ncclSuccess;
-        ok = (ncclGroupEnd() == ncclSuccess) && ok;
-        std::vector<sa_result> all((size_t)G * width);
+            ok = R.gather(sh[s].d_send, s == 0 ? d_gather : nullptr, width * sizeof(sa_result), ncclUint8, 0,
+                          (*comms)[s], sh[s].st) == ncclSuccess;
+        ok = (R.groupEnd() == ncclSuccess) && ok;
+        all.resize((size_t)G * width);
         if (ok)
         {
             (void)hipSetDevice(0);
             ok = hipMemcpyAsync(all.data(), d_gather, all.size() * sizeof(sa_result), hipMemcpyDeviceToHost,
-                                streams[0]) == hipSuccess;
+                                sh[0].st) == hipSuccess;
             for (int s = 0; s < G && ok; ++s)
             {
                 (void)hipSetDevice(s);
-                ok = hipStreamSynchronize(streams[s]) == hipSuccess;
+                ok = hipStreamSynchronize(sh[s].st) == hipSuccess;
             }
         }
-        for (int s = 0; s < G; ++s)
-            if (streams[s])
-            {
-                (void)hipSetDevice(s);
-                (void)hipStreamDestroy(streams[s]);
-            }
         if (!ok)
         {
             release();
             return fail_b(SA_ERR_HIP, "sa_align_batch: RCCL result gather failed");
         }
-        for (int s = 0; s < G; ++s)
-            for (size_t q = 0; q < sh[s].idx.size(); ++q) results[sh[s].idx[q]] = all[(size_t)s * width + q];
+        t_last_gather_ms = ms_since(tg);
+        t_last_rccl = 1;
     }
-    else
+    for (int s = 0; s < G; ++s)
     {
-        for (const Shard &x : sh)
-            for (size_t q = 0; q < x.idx.size(); ++q) results[x.idx[q]] = x.res[q];
+        const Shard &x = sh[s];
+        for (size_t q = 0; q < x.idx.size(); ++q)
+        {
+            const int64_t i = x.idx[q];
+            results[i] = use_rccl ? all[(size_t)s * width + q] : x.res[q];
+            const uint64_t L = results[i].num_alignment_bytes;
+            if (aligned_text && aligned_text[i] && L) std::memcpy(aligned_text[i], &x.ot[x.off[q]], L);
+            if (aligned_pattern && aligned_pattern[i] && L) std::memcpy(aligned_pattern[i], &x.op[x.off[q]], L);
+        }
     }
     release();
     return SA_OK;

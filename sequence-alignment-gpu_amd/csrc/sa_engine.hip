@@ -482,6 +482,9 @@ int ctx_prepare(DeviceCtx *c, size_t bytes)
     if (!c->e1) HIP_TRY(hipEventCreate(&c->e1));
     if (c->arena_bytes < bytes)
     {
+        // grow geometrically (x1.25 of the old size) so a sweep of rising sizes does not reallocate
+        // every call
+        const size_t want = std::max(bytes, c->arena_bytes + c->arena_bytes / 4);
         if (c->arena)
         {
             HIP_TRY(hipStreamSynchronize(c->stream));
@@ -489,8 +492,6 @@ int ctx_prepare(DeviceCtx *c, size_t bytes)
             c->arena = nullptr;
             c->arena_bytes = 0;
         }
-        // grow geometrically (x1.25) so a sweep of rising sizes does not reallocate every call
-        const size_t want = std::max(bytes, c->arena_bytes + c->arena_bytes / 4);
         if (hipMalloc((void **)&c->arena, want) != hipSuccess)
         {
             (void)hipGetLastError();
@@ -1019,7 +1020,7 @@ int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
     if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
     Control ctrl;
     HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
-    if (!pl->pairs.empty())
+    if (out && !pl->pairs.empty())
         HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
@@ -1052,14 +1053,14 @@ uint64_t sa_plan_output_bytes(const sa_plan *pl) { return pl ? pl->out_bytes : 0
 int sa_plan_fetch_all(sa_plan *pl, sa_result *out, char *tb, char *pb, uint64_t buf_bytes, uint64_t *offsets,
                       void *stream)
 {
-    if (!pl || (!pl->pairs.empty() && (!out || !offsets))) return fail(SA_ERR_INVALID, "sa_plan_fetch_all: null argument");
+    if (!pl || (!pl->pairs.empty() && !offsets)) return fail(SA_ERR_INVALID, "sa_plan_fetch_all: null argument");
     if ((tb || pb) && buf_bytes < pl->out_bytes) return fail(SA_ERR_INVALID, "sa_plan_fetch_all: buffers below sa_plan_output_bytes");
     hipStream_t st = (hipStream_t)stream;  // NULL = the HIP null stream
     DeviceGuard dg(pl->device);
     if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
     Control ctrl;
     HIP_TRY(hipMemcpyAsync(&ctrl, pl->d_ctrl, sizeof(Control), hipMemcpyDeviceToHost, st));
-    if (!pl->pairs.empty())
+    if (out && !pl->pairs.empty())
         HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
     if (tb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(tb, pl->d_out_text, pl->out_bytes, hipMemcpyDeviceToHost, st));
     if (pb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(pb, pl->d_out_pattern, pl->out_bytes, hipMemcpyDeviceToHost, st));

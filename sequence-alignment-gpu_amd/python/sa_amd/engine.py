@@ -21,7 +21,8 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
            "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace",
-           "sa_plan_output_bytes", "sa_plan_fetch_all", "sa_align_batch", "sa_batch_deal")
+           "sa_plan_output_bytes", "sa_plan_fetch_all", "sa_align_batch", "sa_batch_deal", "sa_build_id",
+           "sa_batch_last_stats")
 
 
 class SaParams(ctypes.Structure):
@@ -80,9 +81,24 @@ def _load():
     L.sa_plan_fetch_all.argtypes = [P, ctypes.POINTER(SaResult), P, P, U64, P, P]
     L.sa_align_batch.argtypes = [ctypes.POINTER(SaParams), P, ctypes.c_int64, I, ctypes.POINTER(SaResult), P, P]
     L.sa_batch_deal.argtypes = [P, ctypes.c_int64, I, P]
+    L.sa_build_id.restype = ctypes.c_char_p
     for name in EXPORTS:
         getattr(L, name)
+    check_build_id(L)
     return L
+
+
+def check_build_id(L) -> None:
+    """Refuse a library built from other sources than the ones next to it (buildid.py). SA_HIP_LIB
+    (an explicitly chosen experiment build) and SA_ALLOW_STALE=1 skip the check."""
+    from . import buildid
+    if "SA_HIP_LIB" in os.environ or os.environ.get("SA_ALLOW_STALE") == "1":
+        return
+    built = L.sa_build_id().decode()
+    want = buildid.source_hash()
+    if built != want:
+        raise ImportError(f"stale HIP engine: {LIB_PATH} was built from sources {built}, the tree holds {want} "
+                          f"(rebuild: make -C {PKG_ROOT})")
 
 
 lib = _load()

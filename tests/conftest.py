@@ -27,12 +27,25 @@ PROT = "ARNDCQEGHILKMFPSTWYVBZX"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD MI355X GPU (HIP engine parity and perf tests)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
-    # Build the in-tree libraries once if they are missing (the HIP library cross-compiles on CPU).
+    # Build the in-tree libraries if they are missing or were built from other sources (build id, the
+    # HIP library cross-compiles on CPU): a stale binary is never tested silently.
     if not os.path.exists(os.path.join(PKG, "lib", "libsa_hip.so")) or not os.path.exists(
-            os.path.join(PKG, "bin", "alignSequence")):
+            os.path.join(PKG, "bin", "alignSequence")) or _stale():
         subprocess.run(["make", "-s", "-C", PKG, "-j4"], check=True)
     if not os.path.exists(os.path.join(ROOT, "oracle", "_build", "libsa_oracle.so")):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "_build/libsa_oracle.so"], check=True)
+
+
+def _stale() -> bool:
+    """True when lib/libsa_hip.so reports another source hash than this tree's (buildid.py)."""
+    import ctypes
+    from sa_amd import buildid
+    try:
+        L = ctypes.CDLL(os.path.join(PKG, "lib", "libsa_hip.so"))
+        L.sa_build_id.restype = ctypes.c_char_p
+        return L.sa_build_id().decode() != buildid.source_hash()
+    except (OSError, AttributeError):
+        return True
 
 
 def load(name: str):

@@ -60,3 +60,25 @@ def test_synthetic_is_deterministic():
     assert len(m) == 1000 and (m == synthetic.mutate(a, 5, 4, 1000)).all()
     # roughly 88 % of the letters survive unchanged in order
     assert (m[:300] == a[:300]).mean() < 1.0
+
+
+def test_build_id_matches_sources_and_detects_an_edit(tmp_path):
+    """Build provenance: libsa_hip.so reports the hash of the sources it was built from
+    (sa_build_id, python/sa_amd/buildid.py) and the hash changes with any byte of csrc/."""
+    import shutil
+    from sa_amd import buildid
+    L = ctypes.CDLL(os.path.join(PKG, "lib", "libsa_hip.so"))
+    L.sa_build_id.restype = ctypes.c_char_p
+    assert L.sa_build_id().decode() == buildid.source_hash()
+    # a copy of the sources with one byte changed hashes differently
+    pkg2, root2 = tmp_path / "repo" / "sequence-alignment-gpu_amd", tmp_path / "repo"
+    shutil.copytree(os.path.join(PKG, "csrc"), pkg2 / "csrc")
+    shutil.copytree(os.path.join(ROOT, "include"), root2 / "include")
+    shutil.copy(os.path.join(PKG, "Makefile"), pkg2 / "Makefile")
+    same = buildid.source_hash(str(pkg2), str(root2))
+    assert same == buildid.source_hash()
+    f = pkg2 / "csrc" / "sa_walk.h"
+    b = bytearray(f.read_bytes())
+    b[-2] ^= 0x01
+    f.write_bytes(bytes(b))
+    assert buildid.source_hash(str(pkg2), str(root2)) != same
