@@ -643,7 +643,13 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         const int64_t v = P->score_matrix[e] + off2;
         if (v < -128 || v > 127) fits8 = false;
     }
-    if (pl->R == 1) pl->sk = fits8 ? kArr8 : kArr;
+    // kArr8's hand-scheduled bodies keep the direction differences in bytes (sa_fill_steps.inc): every
+    // |M - D|, |left - up| is at most 2 (|S| + 2|g|) (global, shifted domain: every boundary is 0 and
+    // adjacent cells differ by at most max(S + 2g, 0)) or 2 (|S| + |g|) + |g| (local, g >= 0), below
+    // 4 (max|S| + |g|). Local with g < 0 has no such bound: H(i, 1) grows like -g * i next to the
+    // column-0 zeros, so M - D at column 1 (and row 1) leaves the byte range.
+    const bool byte_diffs = 4 * (sabs + std::llabs(g)) <= 127 && !(P->mode == SA_LOCAL && g < 0);
+    if (pl->R == 1) pl->sk = fits8 && byte_diffs ? kArr8 : kArr;
     else pl->sk = (A <= 4 && fits8) ? kProf : kTable;
     if (P->alphabet) std::memcpy(pl->alphabet, P->alphabet, std::min<size_t>(A + 1, 33));
     else for (int c = 0; c <= A; ++c) pl->alphabet[c] = c == A ? '-' : (char)('A' + c);

@@ -296,7 +296,9 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
 // tools/gen_fill_asm.py): Q, Qn, diag and F rotate through the roles with period 4, so after a body
 // of U = 16 steps every value is back in its field (F2 is a spare).
 struct StepRegs {
-    int Q, Qn, diag, F, F2;
+    int Q, Qn, diag, F;
+    int X[8], Y[8], Z[8];  // the plane word's direction differences, one byte per step (DIAG, TOP, STOP)
+    int mk[8];             // mk[g] = 0x80808080 >> g (merge_asm)
     uint32_t acc0, acc1, acc2;
     int bm;      // local: running max of (H << kb) - q over the body
     int T[4];    // text-profile words of the body (4 steps each)
@@ -307,8 +309,10 @@ struct StepRegs {
     int msb;              // 0x80000000 in a VGPR (the bitop3 operand that applies raw tags)
     uint64_t bad;         // HP: lanes 0..U-1 whose feed entry did not carry it
 };
-template <bool LOCAL, bool HN, bool HP>
+template <bool LOCAL, bool HN, bool HP, int HALF>
 __device__ __forceinline__ void steps_asm(StepRegs &r);
+template <bool LOCAL>
+__device__ __forceinline__ void merge_asm(StepRegs &r);
 #include "sa_fill_steps.inc"
 
 // One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
@@ -555,6 +559,16 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     };
     int msbv;  // one VGPR for the strip (the compiler would rematerialize a literal per body)
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
+    // the asm bodies' direction-difference bytes (kept across the two bodies of a plane word) and the
+    // merge masks 0x80808080 >> g (opaque: built once per strip, not rematerialized per word)
+    int dX[8], dY[8], dZ[8], mkv[8];
+    sfor<8>([&](auto Gc) {
+        constexpr int g = decltype(Gc)::value;
+        dX[g] = dY[g] = dZ[g] = 0;
+        int m;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "i"((int)(0x80808080u >> g)));
+        mkv[g] = m;
+    });
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     load_codes(0, TA);
     if constexpr (kAhead == 2) load_codes(U, TB);
@@ -591,9 +605,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             r.Q = Q;
             r.diag = upPrev;
             r.F = F[0];
-            r.acc0 = acc[0][0];
-            r.acc1 = acc[1][0];
-            r.acc2 = acc[2][0];
+            sfor<8>([&](auto Gc) {
+                constexpr int g = decltype(Gc)::value;
+                r.X[g] = dX[g];
+                r.Y[g] = dY[g];
+                if constexpr (LOCAL) r.Z[g] = dZ[g];
+            });
             r.bm = -16;  // below every (H << kb) - q
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
             r.g = g;
@@ -607,7 +624,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             else if constexpr (POS == 2) pub_wait(s0 + U);
             r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
             r.pubtag = ring_tag_raw(s0 - 63);
-            steps_asm<LOCAL, HN, HP>(r);  // with HP: reads the next body's feed after step 12
+            steps_asm<LOCAL, HN, HP, POS & 1>(r);  // with HP: reads the next body's feed after step 12
             if constexpr (HP)
             {
                 pfVal = r.pf;
@@ -617,11 +634,23 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             Q = r.Q;
             upPrev = r.diag;
             F[0] = r.F;
-            acc[0][0] = r.acc0;
-            acc[1][0] = r.acc1;
+            sfor<8>([&](auto Gc) {
+                constexpr int g = decltype(Gc)::value;
+                dX[g] = r.X[g];
+                dY[g] = r.Y[g];
+                if constexpr (LOCAL) dZ[g] = r.Z[g];
+            });
+            if constexpr ((POS & 1) == 1)
+            {
+                // the second half of the plane word: its bits into the plane words for the store below
+                sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
+                merge_asm<LOCAL>(r);
+                acc[0][0] = r.acc0;
+                acc[1][0] = r.acc1;
+                if constexpr (LOCAL) acc[2][0] = r.acc2;
+            }
             if constexpr (LOCAL)
             {
-                acc[2][0] = r.acc2;
                 const int kmask = (1 << kb) - 1;
                 best[0] = max(best[0], r.bm + (kmask - (s0 & kmask)));
             }

@@ -37,15 +37,10 @@ def pytest_configure(config):
 
 
 def _stale() -> bool:
-    """True when lib/libsa_hip.so reports another source hash than this tree's (buildid.py)."""
-    import ctypes
+    """True when lib/libsa_hip.so holds another source hash than this tree's (buildid.py; read from
+    the file, not loaded: loading it before torch would start a second HIP runtime)."""
     from sa_amd import buildid
-    try:
-        L = ctypes.CDLL(os.path.join(PKG, "lib", "libsa_hip.so"))
-        L.sa_build_id.restype = ctypes.c_char_p
-        return L.sa_build_id().decode() != buildid.source_hash()
-    except (OSError, AttributeError):
-        return True
+    return buildid.library_id(os.path.join(PKG, "lib", "libsa_hip.so")) != buildid.source_hash()
 
 
 def load(name: str):

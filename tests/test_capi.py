@@ -70,6 +70,7 @@ def test_build_id_matches_sources_and_detects_an_edit(tmp_path):
     L = ctypes.CDLL(os.path.join(PKG, "lib", "libsa_hip.so"))
     L.sa_build_id.restype = ctypes.c_char_p
     assert L.sa_build_id().decode() == buildid.source_hash()
+    assert buildid.library_id(os.path.join(PKG, "lib", "libsa_hip.so")) == buildid.source_hash()
     # a copy of the sources with one byte changed hashes differently
     pkg2, root2 = tmp_path / "repo" / "sequence-alignment-gpu_amd", tmp_path / "repo"
     shutil.copytree(os.path.join(PKG, "csrc"), pkg2 / "csrc")

@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """Generates sequence-alignment-gpu_amd/csrc/sa_fill_steps.inc: hand-scheduled inline-asm step blocks
 of the R = 1 fill's steady bodies (text profiles as int8 bytes, kArr8), global and local, with and
-without a strip below (HN).
+without a strip below (HN), for the first and the second half of a 32-slot plane word (HALF), plus the
+per-word merge of the direction bits.
 
 Why asm: on gfx950 a DPP instruction must be 2 wait states behind the VALU write of any VGPR it
 reads, and an s_nop costs an issue slot (4 cycles) like a VALU op. Scheduled by the compiler the
 step's two lane moves landed right behind their producers (one to two s_nops per step, plus a
-register copy for the bottom-row register), 13-15 issue slots per step; here every DPP sits at least
-two instructions behind its inputs with independent work in between, so a global step is exactly
-its 9 VALU ops and nothing else.
+register copy for the bottom-row register); here every DPP sits at least two instructions behind its
+inputs with independent work in between, so a step is exactly its VALU ops and nothing else.
 
 One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left, period 4):
     b   Qn = Q shifted down one lane (wave_shl:1), written into the register of F two steps back
@@ -16,15 +16,22 @@ One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left,
     c   Q = F shifted up one lane (wave_shr:1), in place: lane 0 keeps the feed value = `up`
     d   D = diag + sext(score byte)          (SDWA byte select of the text-profile word)
     e   M = max(left, up)                    left = F of the previous step
-    f   t1 = left - up                       -> plane 1 (raw up > left / raw TOP)
-    g   global: F' = max(D, M) | local: X = max(D, M, g), F' = X - g, t2 = F' - 1 (STOP), key
+    f   global: F' = max(D, M) | local: X = max(D, M, g), F' = X - g, key
         (F' goes to the diag register, dead after d)
-    h   t0 = M - D                           -> plane 0 (DIAG)
-    i/j/k  push the sign bits into the plane words (v_alignbit acc, acc, t, 31)
-A global step is its 9 VALU ops with or without a strip below: the queue's bottom-row values run
-one step later than the C++ bodies' (whose Qn takes F of the previous step through a register
-copy, 1 VALU per step), and the publish at the body's end shifts the queue once more with F of the
-step before last in lane 63, which gives the same 16 values (1 VALU per body instead of 16).
+    g   X[t & 7] byte 3 - (t >> 3) = M - D         (SDWA, other bytes kept: sign = DIAG)
+    h   Y[t & 7] byte 3 - (t >> 3) = left - up     (sign = raw "up > left" / raw TOP)
+    i   local: Z[t & 7] byte 3 - (t >> 3) = ffbh(F')  (bit 7 = STOP: ffbh(0) = -1, else <= 31)
+with t the step's slot in its 32-slot plane word. A difference's low byte has the sign of the
+difference when the difference lies in [-128, 127]: the plan uses these bodies only when every
+difference is bounded so (sa_engine.hip, byte_diffs). After the word's 32 steps the eight
+registers of a plane hold its 32 sign bits at bits 7 / 15 / 23 / 31: register g has steps g, 8 + g,
+16 + g, 24 + g in bytes 3, 2, 1, 0, so (X[g] & 0x80808080) >> g puts step t at bit 31 - t, the plane
+word layout (sa_layout.h). The merge costs 15 VALU per plane per word and the sign bits 1 VALU per
+bit: about 2.94 VALU per step for two planes instead of 4 (one subtraction and one v_alignbit per
+bit). A global step is 7 VALU ops (plus the merge) with or without a strip below: the queue's
+bottom-row values run one step later than the C++ bodies' (whose Qn takes F of the previous step
+through a register copy), and the publish at the body's end shifts the queue once more with F of
+the step before last in lane 63, which gives the same 16 values (1 VALU per body instead of 16).
 
 Local keys: key' = (F' << kb) - q, its running maximum bm over the block (one v_max3 per two
 steps: keys alternate between two registers); the caller adds the body's key base
@@ -41,34 +48,16 @@ U = 16
 PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "12"))
 
 
-def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
-    # operand numbers (see the C++ wrapper below)
-    A, B, C = "%0", "%1", "%2"
-    FA, FB = "%3", "%4"
-    D, M, T0, T1 = "%5", "%6", "%7", "%8"
-    ACC0, ACC1 = "%9", "%10"
-    # outputs first (Q .. acc1 = %0..%10, local extras %11..%15, then the feed value and its
-    # bad-lane mask), then inputs (T words, local g / kb, feed address and raw tag, publish address and
-    # raw tag, the sign-bit constant). A raw tag is (c + 63) << 20 of the slot's column c: its bit 31 is
-    # the lap parity, the complement of the tag (sa_fill.hip ring_tag); v_bitop3 applies it.
-    h = 2 if hp else 0
-    nout = (11 if not local else 17) + h
-    PF = f"%{nout - 2}"
-    BAD = f"%{nout - 1}"
-    TW = [f"%{nout + i}" for i in range(4)]
-    k = nout + 4
-    ACC2 = BM = X = T2 = KEY = KEY2 = G = KB = None
-    if local:
-        ACC2, BM, X, T2, KEY, KEY2 = "%11", "%12", "%13", "%14", "%15", "%16"
-        G, KB = f"%{k}", f"%{k + 1}"
-        k += 2
-    PFA, CTAG = f"%{k}", f"%{k + 1}"
-    if hp:
-        k += 2
-    PADDR, PTAG = f"%{k}", f"%{k + 1}"
-    if hn:
-        k += 2
-    MSB = f"%{k}"
+def block(local: bool, hn: bool, hp: bool, half: int) -> str:
+    # named operands (the C++ wrapper below binds them)
+    A, B, C, FA = "%[q]", "%[qn]", "%[dg]", "%[f]"
+    D, M, T0 = "%[d]", "%[m]", "%[t0]"
+    X = [f"%[x{g}]" for g in range(8)]
+    Y = [f"%[y{g}]" for g in range(8)]
+    Z = [f"%[z{g}]" for g in range(8)]
+    TW = [f"%[tw{i}]" for i in range(4)]
+    G, KB, BM, XR, KEY, KEY2 = "%[g]", "%[kb]", "%[bm]", "%[xr]", "%[key]", "%[key2]"
+    PF, BAD, PFA, CTAG, PADDR, PTAG, MSB = "%[pf]", "%[bad]", "%[pfa]", "%[ctag]", "%[paddr]", "%[ptag]", "%[msb]"
     # four registers rotate through the roles with period 4 (U = 16 returns them to their operands):
     # at step k, regs[k % 4] takes the shifted queue (Qn; it held F of step k-2, dead), regs[k-1] is
     # Q (shifted down, then overwritten in place by up), regs[k-2] is diag (then takes F'), regs[k-3]
@@ -78,7 +67,11 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     regs = [B, FA, C, A]  # at entry: regs[3] = Q, regs[1] = F (left), regs[2] = diag, regs[0] dead
     out = []
     out.append("s_nop 1")  # the compiler's last writes of Q / F stand right before
-    for k, q in enumerate(range(qb, qe)):
+    for k in range(U):
+        q = k
+        t = 16 * half + q
+        g, byte = t & 7, 3 - (t >> 3)
+        sd = f"dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
         if hp and q == PF_STEP:
             out.append(f"ds_read_b32 {PF}, {PFA}")
@@ -90,27 +83,21 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
         out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
                    f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
         out.append(f"v_max_i32_e32 {M}, {fp}, {qr}")
-        out.append(f"v_sub_u32_e32 {T1}, {fp}, {qr}")
+        out.append(f"v_sub_u32_sdwa {Y[g]}, {fp}, {qr} {sd}")
         if not local:
             out.append(f"v_max_i32_e32 {dg}, {D}, {M}")
-            out.append(f"v_sub_u32_e32 {T0}, {M}, {D}")
-            out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
-            out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
+            out.append(f"v_sub_u32_sdwa {X[g]}, {M}, {D} {sd}")
         else:
             # H = max(X, g) - g = max(X - g, 0) for g > 0 and X - g (never 0 clamped) for g <= 0
-            out.append(f"v_max3_i32 {X}, {D}, {M}, {G}")
-            out.append(f"v_sub_u32_e32 {T0}, {M}, {D}")
-            out.append(f"v_subrev_u32_e32 {dg}, {G}, {X}")
-            out.append(f"v_alignbit_b32 {ACC1}, {ACC1}, {T1}, 31")
-            out.append(f"v_add_u32_e32 {T2}, -1, {dg}")
+            out.append(f"v_max3_i32 {XR}, {D}, {M}, {G}")
+            out.append(f"v_sub_u32_sdwa {X[g]}, {M}, {D} {sd}")
+            out.append(f"v_subrev_u32_e32 {dg}, {G}, {XR}")
             kreg = KEY if k % 2 == 0 else KEY2
             out.append(f"v_lshl_add_u32 {kreg}, {dg}, {KB}, {-q}")
-            out.append(f"v_alignbit_b32 {ACC0}, {ACC0}, {T0}, 31")
+            # STOP: ffbh(H) is 0xffffffff for H == 0 and at most 31 otherwise: bit 7 of its low byte
+            out.append(f"v_ffbh_u32_sdwa {Z[g]}, {dg} dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD")
             if k % 2 == 1:
                 out.append(f"v_max3_i32 {BM}, {BM}, {KEY}, {KEY2}")
-            out.append(f"v_alignbit_b32 {ACC2}, {ACC2}, {T2}, 31")
-    nst = qe - qb
-    assert nst % 4 == 0, "the register rotation needs whole periods"
     if hp:
         out.append("s_waitcnt lgkmcnt(0)")  # the feed read (issued 4 steps ago) is there
         # tag check: x = entry ^ expected tag (the value when it matches; bitop3 0xD2 = a ^ (~b & c)),
@@ -129,46 +116,82 @@ def block(local: bool, hn: bool, hp: bool, qb: int = 0, qe: int = U) -> str:
     return "\\n\\t".join(out)
 
 
+def merge(local: bool) -> str:
+    """The word's sign bits into the plane words: acc = OR_g (X[g] & 0x80808080) >> g."""
+    out = []
+    planes = [("x", "%[a0]"), ("y", "%[a1]")] + ([("z", "%[a2]")] if local else [])
+    for p, acc in planes:
+        out.append(f"v_and_b32_e32 {acc}, 0x80808080, %[{p}0]")
+    for g in range(1, 8):
+        for p, acc in planes:
+            out.append(f"v_lshrrev_b32_e32 %[t{p}], {g}, %[{p}{g}]")
+            out.append(f"v_and_or_b32 {acc}, %[t{p}], %[mk{g}], {acc}")
+    return "\\n\\t".join(out)
+
+
+def operands(local: bool, hn: bool, hp: bool):
+    outs = ['[q] "+v"(r.Q)', '[qn] "=&v"(r.Qn)', '[dg] "+v"(r.diag)', '[f] "+v"(r.F)',
+            '[d] "=&v"(D)', '[m] "=&v"(M)', '[t0] "=&v"(t0)']
+    outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
+    ins = [f'[tw{i}] "v"(r.T[{i}])' for i in range(4)]
+    if local:
+        outs += [f'[z{g}] "+v"(r.Z[{g}])' for g in range(8)]
+        outs += ['[bm] "+v"(r.bm)', '[xr] "=&v"(Xr)', '[key] "=&v"(key)', '[key2] "=&v"(key2)']
+        ins += ['[g] "s"(r.g)', '[kb] "s"(r.kb)']
+    if hp:
+        # early-clobber: the mask is written before the publish reads its raw tag (an SGPR input the
+        # compiler could otherwise assign to the same register)
+        outs += ['[pf] "=&v"(r.pf)', '[bad] "=&s"(r.bad)']
+        ins += ['[pfa] "v"(r.pfaddr)', '[ctag] "s"(r.ctag)']
+    if hn:
+        ins += ['[paddr] "v"(r.pubaddr)', '[ptag] "s"(r.pubtag)']
+    if hn or hp:
+        ins += ['[msb] "v"(r.msb)']
+    return outs, ins
+
+
 def main():
     lines = [
         "// GENERATED by tools/gen_fill_asm.py -- do not edit. Hand-scheduled steady steps of the R = 1",
         "// kArr8 fill (see the generator's docstring for the schedule and its hazard rules).",
-        "// steps_asm<LOCAL, HN, HP>(r): the U = 16 steps of a body; Q / Qn / diag / F rotate through the",
-        "// roles with period 4 (back in place after the body); with HP the next body's feed read (address",
-        "// r.pfaddr) is issued after step 12 and waited for at the end (result r.pf).",
+        "// steps_asm<LOCAL, HN, HP, HALF>(r): the U = 16 steps of a body (slots 16 * HALF .. 16 * HALF + 15",
+        "// of its plane word); Q / Qn / diag / F rotate through the roles with period 4 (back in place after",
+        "// the body); with HP the next body's feed read (address r.pfaddr) is issued after step 12 and",
+        "// waited for at the end (result r.pf). merge_asm<LOCAL>(r) builds the word's plane words.",
         "#pragma once",
         "",
     ]
     for local in (False, True):
         for hn in (False, True):
             for hp in (False, True):
-                body = block(local, hn, hp)
-                lines.append(f"template <> __device__ __forceinline__ void steps_asm<{str(local).lower()}, "
-                             f"{str(hn).lower()}, {str(hp).lower()}>(StepRegs &r)")
-                lines.append("{")
-                lines.append("    int D, M, t0, t1, X, t2, key, key2;")
-                lines.append(f"    asm volatile(\"{body}\"")
-                lines.append("        : \"+v\"(r.Q), \"=&v\"(r.Qn), \"+v\"(r.diag), \"+v\"(r.F), \"=&v\"(r.F2),")
-                lines.append("          \"=&v\"(D), \"=&v\"(M), \"=&v\"(t0), \"=&v\"(t1), \"+v\"(r.acc0), \"+v\"(r.acc1)")
-                if local:
-                    lines.append("          , \"+v\"(r.acc2), \"+v\"(r.bm), \"=&v\"(X), \"=&v\"(t2), \"=&v\"(key), \"=&v\"(key2)")
-                if hp:
-                    # early-clobber: the mask is written before the publish reads its raw tag (an SGPR
-                    # input the compiler could otherwise assign to the same register)
-                    lines.append("          , \"=&v\"(r.pf), \"=&s\"(r.bad)")
-                ins = "\"v\"(r.T[0]), \"v\"(r.T[1]), \"v\"(r.T[2]), \"v\"(r.T[3])"
-                if local:
-                    ins += ", \"s\"(r.g), \"s\"(r.kb)"
-                if hp:
-                    ins += ", \"v\"(r.pfaddr), \"s\"(r.ctag)"
-                if hn:
-                    ins += ", \"v\"(r.pubaddr), \"s\"(r.pubtag)"
-                if hn or hp:
-                    ins += ", \"v\"(r.msb)"
-                lines.append(f"        : {ins}" + (" : \"scc\");" if hp else ");"))
-                lines.append("    (void)D; (void)M; (void)t0; (void)t1; (void)X; (void)t2; (void)key; (void)key2;")
-                lines.append("}")
-                lines.append("")
+                for half in (0, 1):
+                    body = block(local, hn, hp, half)
+                    outs, ins = operands(local, hn, hp)
+                    lines.append(f"template <> __device__ __forceinline__ void steps_asm<{str(local).lower()}, "
+                                 f"{str(hn).lower()}, {str(hp).lower()}, {half}>(StepRegs &r)")
+                    lines.append("{")
+                    lines.append("    int D, M, t0, Xr, key, key2;")
+                    lines.append(f"    asm volatile(\"{body}\"")
+                    lines.append("        : " + ", ".join(outs))
+                    lines.append("        : " + ", ".join(ins) + (" : \"scc\");" if hp else ");"))
+                    lines.append("    (void)D; (void)M; (void)t0; (void)Xr; (void)key; (void)key2;")
+                    lines.append("}")
+                    lines.append("")
+        outs = ['[a0] "=&v"(r.acc0)', '[a1] "=&v"(r.acc1)', '[tx] "=&v"(tx)', '[ty] "=&v"(ty)']
+        ins = [f'[x{g}] "v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "v"(r.Y[{g}])' for g in range(8)]
+        ins += [f'[mk{g}] "v"(r.mk[{g}])' for g in range(1, 8)]
+        if local:
+            outs += ['[a2] "=&v"(r.acc2)', '[tz] "=&v"(tz)']
+            ins += [f'[z{g}] "v"(r.Z[{g}])' for g in range(8)]
+        lines.append(f"template <> __device__ __forceinline__ void merge_asm<{str(local).lower()}>(StepRegs &r)")
+        lines.append("{")
+        lines.append("    int tx, ty, tz;")
+        lines.append(f"    asm volatile(\"{merge(local)}\"")
+        lines.append("        : " + ", ".join(outs))
+        lines.append("        : " + ", ".join(ins) + ");")
+        lines.append("    (void)tx; (void)ty; (void)tz;")
+        lines.append("}")
+        lines.append("")
     open(OUT, "w").write("\n".join(lines))
     print("wrote", OUT)
 
