@@ -82,6 +82,8 @@ def _load():
     L.sa_align_batch.argtypes = [ctypes.POINTER(SaParams), P, ctypes.c_int64, I, ctypes.POINTER(SaResult), P, P]
     L.sa_batch_deal.argtypes = [P, ctypes.c_int64, I, P]
     L.sa_build_id.restype = ctypes.c_char_p
+    L.sa_batch_last_stats.argtypes = [ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), P,
+                                      ctypes.c_int32, ctypes.POINTER(ctypes.c_double)]
     for name in EXPORTS:
         getattr(L, name)
     check_build_id(L)
@@ -160,6 +162,17 @@ def batch_deal(cells: list[int], num_shards: int) -> list[int]:
     out = np.zeros(max(1, len(c)), np.int32)
     _check(lib.sa_batch_deal(c.ctypes.data, len(c), num_shards, out.ctypes.data))
     return out[: len(c)].tolist()
+
+
+def batch_last_stats() -> dict:
+    """sa_batch_last_stats: the calling thread's last sa_align_batch (shards, RCCL or not, per-shard
+    wall ms from upload to traceback end, gather wall ms)."""
+    ns, rc = ctypes.c_int32(0), ctypes.c_int32(0)
+    ms = np.zeros(64, np.float64)
+    g = ctypes.c_double(0)
+    _check(lib.sa_batch_last_stats(ctypes.byref(ns), ctypes.byref(rc), ms.ctypes.data, 64, ctypes.byref(g)))
+    return {"num_shards": ns.value, "used_rccl": bool(rc.value), "shard_ms": ms[: ns.value].round(3).tolist(),
+            "gather_ms": round(g.value, 3)}
 
 
 def align_batch(mode: int, texts: list[np.ndarray], patterns: list[np.ndarray], S: np.ndarray, gap: int,

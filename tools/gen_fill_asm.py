@@ -32,6 +32,8 @@ bit). A global step is 7 VALU ops (plus the merge) with or without a strip below
 bottom-row values run one step later than the C++ bodies' (whose Qn takes F of the previous step
 through a register copy), and the publish at the body's end shifts the queue once more with F of
 the step before last in lane 63, which gives the same 16 values (1 VALU per body instead of 16).
+(Publishing the first 8 of them after step 8's shift as well does not shorten the hand-off: a
+consumer's feed read takes a whole body's 16 columns, whose last 8 come with the body's end.)
 
 Local keys: key' = (F' << kb) - q, its running maximum bm over the block (one v_max3 per two
 steps: keys alternate between two registers); the caller adds the body's key base
@@ -45,7 +47,7 @@ OUT = os.path.join(ROOT, "sequence-alignment-gpu_amd", "csrc", "sa_fill_steps.in
 
 U = 16
 # with a strip above, the next body's feed read is issued after this step (kPfLead = U - PF_STEP)
-PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "12"))
+PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "14"))
 
 
 def block(local: bool, hn: bool, hp: bool, half: int) -> str:

@@ -1,9 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "gap_pairs_batched or data_pairs_batched" > gpurun_out/t0.log 2>&1; echo "t0 rc=$?"; tail -3 gpurun_out/t0.log
-timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py -m gpu > gpurun_out/t1.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py tests/test_edge_cases.py -m gpu > gpurun_out/t1.log 2>&1
 rc=$?
-tail -5 gpurun_out/t1.log
+tail -3 gpurun_out/t1.log
 [ $rc -eq 0 ] || exit $rc
 for w in headline local dna8k protein4k; do timeout -k 10 120 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/b_$w.json 2> gpurun_out/b_$w.err || exit 1; done
 python - <<'PY'
@@ -12,3 +11,5 @@ for w in ["headline","local","dna8k","protein4k"]:
     d=json.loads(open(f"gpurun_out/b_{w}.json").read().strip().splitlines()[-1])
     print(w, d["value"], d["ms_per_step"], d.get("roofline",{}).get("achieved"), d.get("e2e_ms"))
 PY
+bash tools/gpu_tl.sh
+timeout -k 10 300 python bench.py --workload batch --native --gpus 1 --steps 3 --warmup 1 > gpurun_out/b_native.json 2>gpurun_out/b_native.err && tail -c 600 gpurun_out/b_native.json
