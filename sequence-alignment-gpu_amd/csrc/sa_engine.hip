@@ -967,7 +967,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     DevPtr<uint64_t> tmBuf;
     if (tmPath)
     {
-        HIP_TRY(hipMalloc((void **)&timing, sizeof(uint64_t) * 4 * np));
+        HIP_TRY(hipMalloc((void **)&timing, sizeof(uint64_t) * 8 * np));
         tmBuf.reset(timing);
     }
     // row / column walk (records) + expansion (sa_walk.hip)
@@ -1006,7 +1006,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     if (int rc = debug_sync(st, "expand_kernel")) return rc;
     if (tmPath)
     {
-        std::vector<uint64_t> tm(4 * (size_t)np);
+        std::vector<uint64_t> tm(8 * (size_t)np);
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMemcpy(tm.data(), timing, tm.size() * 8, hipMemcpyDeviceToHost));
         if (FILE *f = std::fopen(tmPath, "wb"))
@@ -1103,11 +1103,22 @@ int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *strea
         const StripDesc &sd = pl->strips[pd.first_strip + b];
         for (uint64_t j = 1; j <= n; ++j)
         {
-            // slot e of the strip: chunk e/CS, lane k's LW words, plane word (e%CS)/32, bit 31-e%32
+            // slot e of the strip: chunk e/CS, lane k's LW words; R = 1: interleaved word (e%32)/16,
+            // bits 31 - 2(e%16) / 30 - 2(e%16); R > 1: plane word (e%CS)/32, bit 31-e%32
             const uint64_t e = (j - 1 + k) * R + rho;
-            const uint32_t *w = &h[(sd.mask_off - e0) * 4 + (e / CS) * kWave * LW + k * LW + (e % CS) / 32];
-            const uint32_t b0 = (w[0] >> (31 - e % 32)) & 1u;
-            const uint32_t b1 = (w[NW] >> (31 - e % 32)) & 1u;
+            const uint32_t *w = &h[(sd.mask_off - e0) * 4 + (e / CS) * kWave * LW + k * LW];
+            uint32_t b0, b1;
+            if (R == 1)
+            {
+                const uint32_t x = w[(e % 32) / 16];
+                b0 = (x >> (31 - 2 * (e % 16))) & 1u;
+                b1 = (x >> (30 - 2 * (e % 16))) & 1u;
+            }
+            else
+            {
+                b0 = (w[(e % CS) / 32] >> (31 - e % 32)) & 1u;
+                b1 = (w[NW + (e % CS) / 32] >> (31 - e % 32)) & 1u;
+            }
             // global: plane1 is the raw "up > left" bit and DIAG wins (see run_body)
             M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
         }

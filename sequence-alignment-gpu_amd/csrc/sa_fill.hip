@@ -234,8 +234,16 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
             }
             const int left = F[rho];
             const int M = max(left, up);
-            acc[0][w] = push_sign(acc[0][w], M - D);      // DIAG
-            acc[1][w] = push_sign(acc[1][w], left - up);  // raw "up > left" (global) / raw TOP (local)
+            if constexpr (R > 1)
+            {
+                acc[0][w] = push_sign(acc[0][w], M - D);      // DIAG
+                acc[1][w] = push_sign(acc[1][w], left - up);  // raw "up > left" (global) / raw TOP (local)
+            }
+            else if constexpr (!LOCAL)
+            {
+                // R = 1: interleaved word, DIAG then raw "up > left" per slot (sa_layout.h)
+                acc[0][0] = push_sign(push_sign(acc[0][0], M - D), left - up);
+            }
             int Fn;
             if constexpr (!LOCAL)
             {
@@ -246,7 +254,13 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 // H = max(X, g) - g: max(X - g, 0) for g > 0, and X - g for g <= 0 (X >= 0)
                 const int X = max(max(D, M), g);
                 Fn = X - g;
-                acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
+                if constexpr (R > 1) acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
+                else
+                {
+                    // interleaved: DIAG|STOP, then (TOP & ~DIAG)|STOP (sign bits: Fn - 1 < 0 iff H == 0)
+                    const int dd = M - D;
+                    acc[0][0] = push_sign(push_sign(acc[0][0], dd | (Fn - 1)), ((left - up) & ~dd) | (Fn - 1));
+                }
                 const int key = (Fn << kb) + Ks;
                 if constexpr (RAMP) best[rho] = act ? max(best[rho], key) : best[rho];
                 else best[rho] = max(best[rho], key);
@@ -264,6 +278,12 @@ template <int R, bool LOCAL>
 __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)[3][Cfg<R>::NW])
 {
     constexpr int NW = Cfg<R>::NW;
+    if constexpr (R == 1)
+    {
+        // interleaved words: slots 0..15 (the chunk's first body), slots 16..31
+        *reinterpret_cast<u32x2 *>(dst) = u32x2{acc[1][0], acc[0][0]};
+        return;
+    }
     uint32_t v[2 * NW];
     sfor<NW>([&](auto Wc) {
         constexpr int w = decltype(Wc)::value;
@@ -298,8 +318,9 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
 struct StepRegs {
     int Q, Qn, diag, F;
     int X[8], Y[8], Z[8];  // the plane word's direction differences, one byte per step (DIAG, TOP, STOP)
-    int mk[8];             // mk[g] = 0x80808080 >> g (merge_asm)
-    uint32_t acc0, acc1, acc2;
+    int mk[8];             // mk[s] = 0x80808080 >> s (merge_asm)
+    int mz[4];             // mz[t] = 0xc0c0c0c0 >> 2t (local STOP bytes to both bits)
+    uint32_t acc0, acc1;   // the chunk's two interleaved words (merge_asm)
     int bm;      // local: running max of (H << kb) - q over the body
     int T[4];    // text-profile words of the body (4 steps each)
     int g, kb;
@@ -561,13 +582,19 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     // the asm bodies' direction-difference bytes (kept across the two bodies of a plane word) and the
     // merge masks 0x80808080 >> g (opaque: built once per strip, not rematerialized per word)
-    int dX[8], dY[8], dZ[8], mkv[8];
+    int dX[8], dY[8], dZ[8], mkv[8], mzv[4];
     sfor<8>([&](auto Gc) {
         constexpr int g = decltype(Gc)::value;
         dX[g] = dY[g] = dZ[g] = 0;
         int m;
         asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "i"((int)(0x80808080u >> g)));
         mkv[g] = m;
+    });
+    sfor<4>([&](auto Tc) {
+        constexpr int t = decltype(Tc)::value;
+        int m = 0;
+        if constexpr (LOCAL) asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "i"((int)(0xc0c0c0c0u >> (2 * t))));
+        mzv[t] = m;
     });
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     load_codes(0, TA);
@@ -642,12 +669,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             });
             if constexpr ((POS & 1) == 1)
             {
-                // the second half of the plane word: its bits into the plane words for the store below
+                // the chunk's second body: its bits into the two interleaved words for the store below
                 sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
+                if constexpr (LOCAL) sfor<4>([&](auto Tc) { r.mz[decltype(Tc)::value] = mzv[decltype(Tc)::value]; });
                 merge_asm<LOCAL>(r);
-                acc[0][0] = r.acc0;
-                acc[1][0] = r.acc1;
-                if constexpr (LOCAL) acc[2][0] = r.acc2;
+                acc[1][0] = r.acc0;
+                acc[0][0] = r.acc1;
             }
             if constexpr (LOCAL)
             {
@@ -660,6 +687,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
             run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
             prefetch(s1);
             run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+            // R = 1: a body fills one interleaved word; the chunk's first word waits in acc[1][0]
+            if constexpr (R == 1 && !second::value) acc[1][0] = acc[0][0];
         }
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STORE)
         if constexpr (false)  // timing ablation: no direction planes are written

@@ -13,7 +13,10 @@
 // words}, each word 32 consecutive slots with the first slot in bit 31. So slot e of lane k is bit
 // 31 - e%32 of dword  c*64*LW + k*LW + P*(CS/32) + (e%CS)/32  (c = e/CS, plane P) from the strip's
 // base  masks + 16*strip.mask_off  bytes. That is 16 bytes per slot, and a range of slots that
-// starts on a chunk boundary is a contiguous byte range. The reference DIRECTION code (LEFT=0,
+// starts on a chunk boundary is a contiguous byte range. R = 1 (CS = 32, LW = 2) INTERLEAVES the
+// planes instead: lane k's two dwords of chunk c are slots 32c .. 32c+15 and 32c+16 .. 32c+31, slot
+// e at bits 31 - 2(e%16) (plane0) and 30 - 2(e%16) (plane1) of dword (e%32)/16, so the traceback's
+// row windows (two bits per cell) are funnel shifts of the lane's stream. The reference DIRECTION code (LEFT=0,
 // DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) is
 //   global: plane0 = DIAG, plane1 = "up > left";  code = plane0 ? DIAG : plane1 ? TOP : LEFT
 //   local:  plane0 = DIAG|STOP, plane1 = (TOP&~DIAG)|STOP;  code = plane0 | plane1 << 1

@@ -24,8 +24,8 @@
 // row 0 LEFT; local: STOP), so they need no tests.
 //
 // ROW WALK (R = 1): lanes = the 64 rows of a strip (lane k = row k), windows = 8 x 16 columns left of
-//   the strip's entry column, built from the lane's own plane words (sa_layout.h: R = 1 slot e =
-//   j - 1 + k) by funnel shifts and bit interleaving. While a strip is walked, the raw planes of the
+//   the strip's entry column, funnel shifts of the lane's own interleaved plane words (sa_layout.h:
+//   R = 1 slot e = j - 1 + k). While a strip is walked, the raw planes of the
 //   strip above, around the predicted entry column, are copied to LDS by global_load_lds, so staging
 //   reads LDS, not HBM.
 // COLUMN WALK (R >= 2, the batch shapes): lanes = 64 consecutive columns (lane l = column J0 - 63 + l),
@@ -80,61 +80,63 @@ __device__ __forceinline__ uint32_t window(uint32_t E, uint32_t D) { return spre
 // staging
 // ------------------------------------------------------------------------------------------------
 // Row walk: the eight windows of the calling lane's row (strip row = lane) for origin column jo:
-// window w, bit pair c = column jo - 16w - c. Raw plane words come from the LDS prefetch when it covers
-// every lane's chunks, else from global memory (uniform decision). sb = the strip's first dword.
+// window w, bit pair c = column jo - 16w - c. The R = 1 planes are interleaved (sa_layout.h): the lane's
+// dword stream holds each slot's (plane0, plane1) bits as the (odd, even) bits of a pair, slots
+// ascending with the column from bit 31 down, so a window is one funnel shift of two consecutive
+// dwords. Raw plane words come from the LDS prefetch when it covers every lane's chunks, else from
+// global memory (uniform decision). sb = the strip's first dword.
 template <bool LOCAL>
 __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const uint32_t *pf, int pfclo, int jo,
-                                         int lane, uint32_t (&W)[8])
+                                         int lane, uint32_t (&W)[8], uint64_t *dbg = nullptr)
 {
     const int etop = jo - 1 + lane;   // slot of column jo in this lane's stream (R = 1: e = j - 1 + k)
-    const int c0 = etop >> 5;         // (arithmetic shift: etop >= -1)
-    const int b0 = 31 - (etop & 31);  // bit of slot etop in its word (a word's first slot is bit 31)
-    uint32_t r0[5], r1[5];
+    const int c0 = etop >> 5;         // (arithmetic shift: etop may be negative after a restage)
+    const bool hi = (etop & 16) != 0;  // slot etop lies in its chunk's second dword
+    const int sh = 30 - 2 * (etop & 15);  // its pair down to bits 1:0
+    uint32_t L[10];                   // dwords 2c0+1, 2c0, 2c0-1, ..., 2c0-8 of the stream
     const int needLo = max(0, (jo - 1 - 128) >> 5), needHi = (jo + 62) >> 5;
-    if (pfclo != INT_MIN && needLo >= pfclo && needHi < pfclo + kPfChunks)
-    {
-        sfor<5>([&](auto Qc) {
-            constexpr int q = decltype(Qc)::value;
-            const int c = c0 - q;
-            const u32x2 v = *reinterpret_cast<const u32x2 *>(pf + max(c - pfclo, 0) * kChunkDw + lane * 2);
-            r0[q] = c >= 0 ? v.x : 0u;
-            r1[q] = c >= 0 ? v.y : 0u;
-        });
-    }
-    else
-    {
-        sfor<5>([&](auto Qc) {
-            constexpr int q = decltype(Qc)::value;
-            const int c = c0 - q;
-            const u32x2 v = *reinterpret_cast<const u32x2 *>(sb + (int64_t)max(c, 0) * kChunkDw + lane * 2);
-            r0[q] = c >= 0 ? v.x : 0u;
-            r1[q] = c >= 0 ? v.y : 0u;
-        });
-    }
-    sfor<4>([&](auto Sc) {
-        constexpr int s = decltype(Sc)::value;
-        // 32 columns jo - 32s - t (bit t): the slots continue from word c0-s into word c0-s-1
-        const uint32_t X = __builtin_amdgcn_alignbit(r0[s + 1], r0[s], b0);
-        const uint32_t Y = __builtin_amdgcn_alignbit(r1[s + 1], r1[s], b0);
-        const int z = jo - 32 * s;  // column of bit 0 (uniform): bits t < z are columns >= 1
-        const uint32_t vm = z >= 32 ? ~0u : (z <= 0 ? 0u : ((1u << z) - 1u));
-        const uint32_t c0b = (z >= 0 && z < 32) ? (1u << z) : 0u;  // column 0
-        uint32_t T, D;
-        if constexpr (!LOCAL)
-        {
-            D = X & vm;                     // plane 0 = DIAG
-            T = (Y & ~X & vm) | c0b;        // TOP = "up > left" and not DIAG; column 0: TOP (:78-79)
-        }
-        else
-        {
-            // plane 0 = DIAG or STOP, plane 1 = TOP or STOP: STOP (both) sets both bits, and so does
-            // column 0 (the border ends the walk)
-            D = (X & vm) | c0b;
-            T = (Y & vm) | c0b;
-        }
-        W[2 * s] = window(T, D);
-        W[2 * s + 1] = window(T >> 16, D >> 16);
+    const bool inPf = pfclo != INT_MIN && needLo >= pfclo && needHi < pfclo + kPfChunks;
+    sfor<5>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int c = c0 - q;
+        const u32x2 v = inPf ? *reinterpret_cast<const u32x2 *>(pf + max(c - pfclo, 0) * kChunkDw + lane * 2)
+                             : *reinterpret_cast<const u32x2 *>(sb + (int64_t)max(c, 0) * kChunkDw + lane * 2);
+        L[2 * q] = c >= 0 ? v.y : 0u;
+        L[2 * q + 1] = c >= 0 ? v.x : 0u;
     });
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+    if (dbg)
+    {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" : "+v"(L[0]), "+v"(L[9]));
+        dbg[0] += __builtin_amdgcn_s_memtime();  // minus the caller's start stamp
+        dbg[1] += inPf ? 0 : 1;
+    }
+#endif
+    uint32_t S[9];  // S[i] = the dword i before slot etop's
+    sfor<9>([&](auto Ic) {
+        constexpr int i = decltype(Ic)::value;
+        S[i] = hi ? L[i] : L[i + 1];
+    });
+    sfor<8>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        uint32_t x = __builtin_amdgcn_alignbit(S[w + 1], S[w], sh);
+        // global: the even bit is raw "up > left"; a run ends with TOP only without DIAG (:78-79).
+        // local: plane0 = DIAG|STOP and plane1 = (TOP&~DIAG)|STOP are the window bits as they are
+        if constexpr (!LOCAL) x &= ~((x >> 1) & 0x55555555u);
+        W[w] = x;
+    });
+    if (jo < 16 * 8 + 1)
+    {
+        // the windows reach column 0: columns < 1 are cleared, column 0 is TOP (global, :78-79) or
+        // both bits (local: the border ends the walk)
+        sfor<8>([&](auto Wc) {
+            constexpr int w = decltype(Wc)::value;
+            const int z = jo - 16 * w;  // pair of column 0 (uniform)
+            const uint32_t vm = z >= 16 ? ~0u : (z <= 0 ? 0u : ((1u << (2 * z)) - 1u));
+            const uint32_t c0b = (z >= 0 && z < 16) ? (LOCAL ? 3u : 1u) << (2 * z) : 0u;
+            W[w] = (W[w] & vm) | c0b;
+        });
+    }
 }
 
 // Column walk: the eight windows of the calling lane's column j = J0 - 63 + lane for the row blocks
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
         const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
         uint64_t tStage = 0, tBatch = 0;  // shader clocks in staging / in the walk proper
+        uint64_t sdbg[2] = {0, 0}, tLoadStart = 0, nStrips = 0, nRestage = 0;
 #endif
         while (b >= 0)
         {
@@ -470,7 +473,13 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             const uint64_t c0 = __builtin_amdgcn_s_memtime();
 #endif
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+            tLoadStart += c0;
+            ++nStrips;
+            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, sdbg);
+#else
             rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W);
+#endif
             // the windows are complete before the prefetch below is issued: otherwise the wait for
             // the staging loads (vmcnt) would also wait for the prefetch
             asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
@@ -498,6 +507,9 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
                 jo -= 16 * L.na;  // the eight windows are exhausted: the next 128 columns
                 L.na = 0;
                 L.u = 0;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+                ++nRestage;
+#endif
                 rw_stage<LOCAL>(sb, pfbuf[pfb], INT_MIN, jo, lane, W);
             };
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
@@ -545,6 +557,11 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
         {
             a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p] = tStage;
             a.timing[2 * (size_t)gridDim.x + 2 * (size_t)p + 1] = tBatch;
+            // staging load wait, strips staged from global memory (prefetch missed), strips, restages
+            a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p] = sdbg[0] - tLoadStart;
+            a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 1] = sdbg[1];
+            a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 2] = nStrips;
+            a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 3] = nRestage;
         }
 #endif
         if (!L.stopped)

@@ -19,5 +19,7 @@ for f in sa_engine sa_walk sa_batch fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fil
 done
 for p in "${pids[@]}"; do wait $p; done
 mkdir -p $root/build_exp
-/opt/rocm/bin/hipcc $flags -shared $out/*.o -L/opt/rocm/lib -lrccl -o $root/build_exp/libsa_$tag.so
+cp $root/sequence-alignment-gpu_amd/build/build_id.o $out/build_id.o
+/opt/rocm/bin/hipcc $flags -shared $out/*.o -L/opt/rocm/lib -ldl -o $root/build_exp/libsa_$tag.so
+rm -f $root/build_exp/libsa_$tag.so.[0-9]*
 echo built build_exp/libsa_$tag.so

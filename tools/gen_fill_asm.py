@@ -18,17 +18,20 @@ One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left,
     e   M = max(left, up)                    left = F of the previous step
     f   global: F' = max(D, M) | local: X = max(D, M, g), F' = X - g, key
         (F' goes to the diag register, dead after d)
-    g   X[t & 7] byte 3 - (t >> 3) = M - D         (SDWA, other bytes kept: sign = DIAG)
-    h   Y[t & 7] byte 3 - (t >> 3) = left - up     (sign = raw "up > left" / raw TOP)
-    i   local: Z[t & 7] byte 3 - (t >> 3) = ffbh(F')  (bit 7 = STOP: ffbh(0) = -1, else <= 31)
-with t the step's slot in its 32-slot plane word. A difference's low byte has the sign of the
-difference when the difference lies in [-128, 127]: the plan uses these bodies only when every
-difference is bounded so (sa_engine.hip, byte_diffs). After the word's 32 steps the eight
-registers of a plane hold its 32 sign bits at bits 7 / 15 / 23 / 31: register g has steps g, 8 + g,
-16 + g, 24 + g in bytes 3, 2, 1, 0, so (X[g] & 0x80808080) >> g puts step t at bit 31 - t, the plane
-word layout (sa_layout.h). The merge costs 15 VALU per plane per word and the sign bits 1 VALU per
-bit: about 2.94 VALU per step for two planes instead of 4 (one subtraction and one v_alignbit per
-bit). A global step is 7 VALU ops (plus the merge) with or without a strip below: the queue's
+    g   X[4h + (k & 3)] byte 3 - (k >> 2) = M - D     (SDWA, other bytes kept: sign = DIAG)
+    h   Y[4h + (k & 3)] byte 3 - (k >> 2) = left - up  (sign = raw "up > left" / raw TOP)
+    i   local: Z[4h + (k & 3)] byte 3 - (k >> 2) = ffbh(F')  (0xff = STOP: ffbh(0) = -1, else <= 31)
+with k the step in the body and h = HALF the body's word of the 32-slot chunk. A difference's low
+byte has the sign of the difference when the difference lies in [-128, 127]: the plan uses these
+bodies only when every difference is bounded so (sa_engine.hip, byte_diffs). The R = 1 plane word
+is INTERLEAVED (sa_layout.h): slot k of a word has DIAG at bit 31 - 2k and the second plane at bit
+30 - 2k, so register r = 4h + t0 (steps t0, t0 + 4, t0 + 8, t0 + 12 in bytes 3..0) lands with one
+shift: (X[r] & 0x80808080) >> 2 t0, (Y[r] & 0x80808080) >> (2 t0 + 1). The merge costs 15 VALU per
+word (global) and the sign bits 1 VALU per bit: about 2.94 VALU per step for two bits instead of 4
+(one subtraction and one v_alignbit per bit). Local: STOP bytes are 0xff, so (Z & 0xc0c0c0c0) >> 2 t0
+sets both bits of a STOP cell, and word = A | (B & ~(A >> 1)) with A = DIAG|STOP (odd bits) + STOP
+(even bits) and B = raw TOP (even bits) is plane 1 = (TOP & ~DIAG) | STOP: 24 VALU per word.
+A global step is 7 VALU ops (plus the merge) with or without a strip below: the queue's
 bottom-row values run one step later than the C++ bodies' (whose Qn takes F of the previous step
 through a register copy), and the publish at the body's end shifts the queue once more with F of
 the step before last in lane 63, which gives the same 16 values (1 VALU per body instead of 16).
@@ -71,8 +74,7 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
     out.append("s_nop 1")  # the compiler's last writes of Q / F stand right before
     for k in range(U):
         q = k
-        t = 16 * half + q
-        g, byte = t & 7, 3 - (t >> 3)
+        g, byte = 4 * half + (q & 3), 3 - (q >> 2)
         sd = f"dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
         if hp and q == PF_STEP:
@@ -119,15 +121,36 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
 
 
 def merge(local: bool) -> str:
-    """The word's sign bits into the plane words: acc = OR_g (X[g] & 0x80808080) >> g."""
+    """The chunk's sign bits into its two interleaved words a0 (slots 0..15), a1 (slots 16..31)."""
     out = []
-    planes = [("x", "%[a0]"), ("y", "%[a1]")] + ([("z", "%[a2]")] if local else [])
-    for p, acc in planes:
-        out.append(f"v_and_b32_e32 {acc}, 0x80808080, %[{p}0]")
-    for g in range(1, 8):
-        for p, acc in planes:
-            out.append(f"v_lshrrev_b32_e32 %[t{p}], {g}, %[{p}{g}]")
-            out.append(f"v_and_or_b32 {acc}, %[t{p}], %[mk{g}], {acc}")
+    for h, acc in ((0, "%[a0]"), (1, "%[a1]")):
+        # (register, shift, mask operand) terms of the word's DIAG|STOP accumulator and of its TOP one
+        odd = [(f"%[x{4 * h + t0}]", 2 * t0, f"%[mk{2 * t0}]") for t0 in range(4)]
+        if local:
+            odd += [(f"%[z{4 * h + t0}]", 2 * t0, f"%[mz{t0}]") for t0 in range(4)]
+        even = [(f"%[y{4 * h + t0}]", 2 * t0 + 1, f"%[mk{2 * t0 + 1}]") for t0 in range(4)]
+        if not local:
+            terms = [(odd + even, acc)]
+        else:
+            terms = [(odd, acc), (even, "%[tb]")]
+        for lst, a in terms:
+            first = True
+            for reg, sh, mk in lst:
+                if first and sh == 0:
+                    out.append(f"v_and_b32_e32 {a}, 0x80808080, {reg}")
+                elif first:
+                    out.append(f"v_lshrrev_b32_e32 %[tx], {sh}, {reg}")
+                    out.append(f"v_and_b32_e32 {a}, %[tx], {mk}")
+                elif sh == 0:
+                    out.append(f"v_and_or_b32 {a}, {reg}, {mk}, {a}")
+                else:
+                    out.append(f"v_lshrrev_b32_e32 %[tx], {sh}, {reg}")
+                    out.append(f"v_and_or_b32 {a}, %[tx], {mk}, {a}")
+                first = False
+        if local:
+            # plane 1 = (TOP & ~DIAG) | STOP = B & ~(A >> 1) at the even bits (A >> 1 = DIAG|STOP there)
+            out.append(f"v_lshrrev_b32_e32 %[tx], 1, {acc}")
+            out.append(f"v_bitop3_b32 {acc}, %[tb], %[tx], {acc} bitop3:0xba")  # c | (a & ~b)
     return "\\n\\t".join(out)
 
 
@@ -157,9 +180,9 @@ def main():
         "// GENERATED by tools/gen_fill_asm.py -- do not edit. Hand-scheduled steady steps of the R = 1",
         "// kArr8 fill (see the generator's docstring for the schedule and its hazard rules).",
         "// steps_asm<LOCAL, HN, HP, HALF>(r): the U = 16 steps of a body (slots 16 * HALF .. 16 * HALF + 15",
-        "// of its plane word); Q / Qn / diag / F rotate through the roles with period 4 (back in place after",
+        "// of its chunk); Q / Qn / diag / F rotate through the roles with period 4 (back in place after",
         "// the body); with HP the next body's feed read (address r.pfaddr) is issued after step 12 and",
-        "// waited for at the end (result r.pf). merge_asm<LOCAL>(r) builds the word's plane words.",
+        "// waited for at the end (result r.pf). merge_asm<LOCAL>(r) builds the chunk's two words.",
         "#pragma once",
         "",
     ]
@@ -179,19 +202,19 @@ def main():
                     lines.append("    (void)D; (void)M; (void)t0; (void)Xr; (void)key; (void)key2;")
                     lines.append("}")
                     lines.append("")
-        outs = ['[a0] "=&v"(r.acc0)', '[a1] "=&v"(r.acc1)', '[tx] "=&v"(tx)', '[ty] "=&v"(ty)']
+        outs = ['[a0] "=&v"(r.acc0)', '[a1] "=&v"(r.acc1)', '[tx] "=&v"(tx)']
         ins = [f'[x{g}] "v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "v"(r.Y[{g}])' for g in range(8)]
-        ins += [f'[mk{g}] "v"(r.mk[{g}])' for g in range(1, 8)]
+        ins += [f'[mk{g}] "v"(r.mk[{g}])' for g in range(8)]
         if local:
-            outs += ['[a2] "=&v"(r.acc2)', '[tz] "=&v"(tz)']
-            ins += [f'[z{g}] "v"(r.Z[{g}])' for g in range(8)]
+            outs += ['[tb] "=&v"(tb)']
+            ins += [f'[z{g}] "v"(r.Z[{g}])' for g in range(8)] + [f'[mz{t}] "v"(r.mz[{t}])' for t in range(4)]
         lines.append(f"template <> __device__ __forceinline__ void merge_asm<{str(local).lower()}>(StepRegs &r)")
         lines.append("{")
-        lines.append("    int tx, ty, tz;")
+        lines.append("    int tx, tb;")
         lines.append(f"    asm volatile(\"{merge(local)}\"")
         lines.append("        : " + ", ".join(outs))
         lines.append("        : " + ", ".join(ins) + ");")
-        lines.append("    (void)tx; (void)ty; (void)tz;")
+        lines.append("    (void)tx; (void)tb;")
         lines.append("}")
         lines.append("")
     open(OUT, "w").write("\n".join(lines))

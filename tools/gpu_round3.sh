@@ -9,7 +9,7 @@ python - <<'PY'
 import json
 for w in ["headline","local","dna8k","protein4k"]:
     d=json.loads(open(f"gpurun_out/b_{w}.json").read().strip().splitlines()[-1])
-    print(w, d["value"], d["ms_per_step"], d.get("roofline",{}).get("achieved"), d.get("e2e_ms"))
+    print(w, d["value"], d["ms_per_step"], d.get("e2e_ms"), d.get("gcups_fill_plus_traceback"))
 PY
 bash tools/gpu_tl.sh
 timeout -k 10 300 python bench.py --workload batch --native --gpus 1 --steps 3 --warmup 1 > gpurun_out/b_native.json 2>gpurun_out/b_native.err && tail -c 600 gpurun_out/b_native.json

@@ -35,5 +35,8 @@ rec = {"n": args.n, "m": args.m, "mode": args.mode, "ops": r["num_bytes"], "walk
 if len(tm) >= 4 and tm[2] > 0:
     # experiment builds with SA_EXP_WALK_TIMING: shader clocks in staging / in the row walk proper
     rec.update({"stage_clk_per_row": round(tm[2] / args.m, 1), "batch_clk_per_row": round(tm[3] / args.m, 1)})
+    if len(tm) >= 8 and tm[6] > 0:
+        rec.update({"stage_load_clk_per_strip": round(tm[4] / tm[6], 1), "pf_miss": int(tm[5]),
+                    "strips": int(tm[6]), "restages": int(tm[7])})
 print(rec)
 b.close()
