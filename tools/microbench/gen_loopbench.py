@@ -30,7 +30,7 @@ SB, MB = "s[40:41]", "s[42:43]"
 SCNT, SP, SP2, SBODY, SNEED = "s44", "s45", "s46", "s47", "s48"
 SMASK = [None] + [f"s{48 + g}" for g in range(1, 8)]  # s49..s55
 VREGS_USED = 147
-SREGS = list(range(40, 56))
+SREGS = list(range(40, 60))
 
 
 def body(bank_s: int, bank_m: int, word_half: int, bi: int, variant: int, store_pending: bool = True, feat: int = 15) -> list[str]:
@@ -55,10 +55,17 @@ def body(bank_s: int, bank_m: int, word_half: int, bi: int, variant: int, store_
             e(f"s_add_u32 {SP2}, {SP}, 64")
             e(f"s_and_b32 {SP2}, {SP2}, 0x1fff")
         if q < 4 and feat & 1:
+            pass
+        if q < 4 and feat & 1:
             e(f"global_load_dwordx4 v[{S[nb_s][4 * q][1:]}:{int(S[nb_s][4 * q][1:]) + 3}], {VSOFF}, {SB} offset:{128 + 16 * q}")
         if q == 4:
-            e("s_add_u32 s40, s40, 64")
-            e("s_addc_u32 s41, s41, 0")
+            if feat & 256:
+                e("s_add_u32 s56, s56, 64")
+                e("s_and_b32 s56, s56, 0x1fff")
+                e("s_add_u32 s40, s57, s56")
+            else:
+                e("s_add_u32 s40, s40, 64")
+                e("s_addc_u32 s41, s41, 0")
             e(f"v_add_u32_e32 {VFEED}, {SP2}, {VRIN}")
             if word_half == 0 and store_pending and feat & 4:
                 # the previous word's store, issued after this body's loads: the end-of-body wait
@@ -66,12 +73,16 @@ def body(bank_s: int, bank_m: int, word_half: int, bi: int, variant: int, store_
                 e(f"global_store_dwordx2 {VMOFF}, v[{ACC[0][1:]}:{ACC[1][1:]}], {MB}")
                 e("s_add_u32 s42, s42, 512")
                 e("s_addc_u32 s43, s43, 0")
-        if q in (2, 6, 10, 14) and feat & 2:
+        if q in (2, 6, 10, 14) and (feat & 2 or feat & 32):
+            if feat & 64:
+                e("s_mov_b64 exec, s[58:59]")
             e(f"ds_write_b128 {VPUB}, v[{F[0][1:]}:{int(F[0][1:]) + 3}] offset:{16 * (q >> 2)}")
+            if feat & 64:
+                e("s_mov_b64 exec, -1")
         if q == 14 and variant == 2:
             e(f"v_mov_b32_e32 {VPROG}, {SBODY}")
             e(f"ds_write_b32 {VPADDR}, {VPROG} offset:4")
-        if q == 9 and feat & 2:
+        if q == (4 if feat & 128 else 9) and (feat & 2 or feat & 16):
             if variant == 2:
                 e(f"ds_read_b32 {VPRR}, {VPADDR}")
             for j in range(4):
@@ -127,7 +138,8 @@ def slow_paths(variant: int, nb: int) -> list[str]:
 def loop(variant: int, feat: int = 15) -> str:
     lines = [f"s_mov_b32 {SCNT}, %[iters]"]
     lines += [f"s_mov_b32 {SMASK[g]}, 0x{(0x80808080 >> g):08x}" for g in range(1, 8)]
-    lines += ["s_mov_b64 s[40:41], %[sb]", "s_mov_b64 s[42:43], %[mb]", f"s_mov_b32 {SP}, %[sp0]",
+    lines += ["s_mov_b32 s56, 0", "s_mov_b32 s58, 0", "s_mov_b32 s59, 0x80000000",
+              "s_mov_b64 s[40:41], %[sb]", "s_mov_b32 s57, s40", "s_mov_b64 s[42:43], %[mb]", f"s_mov_b32 {SP}, %[sp0]",
               f"s_mov_b32 {SNEED}, %[sneed]", f"s_mov_b32 {SBODY}, 0",
               f"v_mov_b32 {VSOFF}, %[vsoff]", f"v_mov_b32 {VMOFF}, %[vmoff]", f"v_mov_b32 {VLMASK}, %[vlmask]",
               f"v_mov_b32 {VPUBBASE}, %[vpubbase]", f"v_mov_b32 {VRIN}, %[vrin]", f"v_mov_b32 {VPADDR}, %[vpaddr]",
@@ -143,6 +155,11 @@ def loop(variant: int, feat: int = 15) -> str:
     return "\\n\\t".join(x for x in lines if x)
 
 
+FEATS = {"NONE": 0, "LDS": 2, "LDSR": 16, "LDSW": 32, "LDSWX": 32 | 64, "LDSX": 2 | 64, "LDSEARLY": 2 | 128,
+         "LDSEARLYX": 2 | 128 | 64, "LOADS": 1, "LOADSL2": 1 | 256, "ALL_L2": 1 | 2 | 4 | 8 | 256,
+         "ALL_L2X": 1 | 2 | 4 | 8 | 256 | 64 | 128}
+
+
 def main():
     clob = ", ".join(f'"v{i}"' for i in range(32, 32 + VREGS_USED - 32 + 1))
     sclob = ", ".join(f'"s{i}"' for i in SREGS)
@@ -151,8 +168,8 @@ def main():
         f.write(f"#define LB_VCLOB {clob}\n#define LB_SCLOB {sclob}\n")
         for v in range(3):
             f.write(f"#define LB_LOOP{v} \"{loop(v)}\"\n")
-        for ft in range(16):
-            f.write(f"#define LB_FEAT{ft} \"{loop(0, ft)}\"\n")
+        for name, ft in FEATS.items():
+            f.write(f"#define LB_{name} \"{loop(0, ft)}\"\n")
     print("ok")
 
 

@@ -38,13 +38,18 @@ __global__ __launch_bounds__(320) void loop_kernel(const int *sbuf, uint32_t *pl
         if constexpr (V == 0) LB_CALL(LB_LOOP0);
         else if constexpr (V == 1) LB_CALL(LB_LOOP1);
         else if constexpr (V == 2) LB_CALL(LB_LOOP2);
-        else if constexpr (V == 100) LB_CALL(LB_FEAT0);
-        else if constexpr (V == 101) LB_CALL(LB_FEAT1);
-        else if constexpr (V == 102) LB_CALL(LB_FEAT2);
-        else if constexpr (V == 104) LB_CALL(LB_FEAT4);
-        else if constexpr (V == 108) LB_CALL(LB_FEAT8);
-        else if constexpr (V == 110) LB_CALL(LB_FEAT10);
-        else if constexpr (V == 114) LB_CALL(LB_FEAT14);
+        else if constexpr (V == 100) LB_CALL(LB_NONE);
+        else if constexpr (V == 101) LB_CALL(LB_LDS);
+        else if constexpr (V == 102) LB_CALL(LB_LDSR);
+        else if constexpr (V == 103) LB_CALL(LB_LDSW);
+        else if constexpr (V == 104) LB_CALL(LB_LDSWX);
+        else if constexpr (V == 105) LB_CALL(LB_LDSX);
+        else if constexpr (V == 106) LB_CALL(LB_LDSEARLY);
+        else if constexpr (V == 107) LB_CALL(LB_LDSEARLYX);
+        else if constexpr (V == 108) LB_CALL(LB_LOADS);
+        else if constexpr (V == 109) LB_CALL(LB_LOADSL2);
+        else if constexpr (V == 110) LB_CALL(LB_ALL_L2);
+        else if constexpr (V == 111) LB_CALL(LB_ALL_L2X);
     }
     else if (V == 1)
     {
@@ -86,16 +91,18 @@ int main()
     (void)hipMalloc(&out, sizeof(long long) * 256 * 8);
     for (int grid : {1, 132})
     {
-        run<100>("feat_none", grid, s, p, out);
-        run<101>("feat_loads", grid, s, p, out);
-        run<102>("feat_lds", grid, s, p, out);
-        run<104>("feat_store", grid, s, p, out);
-        run<108>("feat_merge", grid, s, p, out);
-        run<110>("feat_lds_merge", grid, s, p, out);
-        run<114>("feat_lds_store_merge", grid, s, p, out);
-        run<0>("nosync", grid, s, p, out);
-        run<1>("barrier8", grid, s, p, out);
-        run<2>("progress16", grid, s, p, out);
+        run<100>("NONE", grid, s, p, out);
+        run<101>("LDS", grid, s, p, out);
+        run<102>("LDSR", grid, s, p, out);
+        run<103>("LDSW", grid, s, p, out);
+        run<104>("LDSWX", grid, s, p, out);
+        run<105>("LDSX", grid, s, p, out);
+        run<106>("LDSEARLY", grid, s, p, out);
+        run<107>("LDSEARLYX", grid, s, p, out);
+        run<108>("LOADS", grid, s, p, out);
+        run<109>("LOADSL2", grid, s, p, out);
+        run<110>("ALL_L2", grid, s, p, out);
+        run<111>("ALL_L2X", grid, s, p, out);
     }
     return 0;
 }
