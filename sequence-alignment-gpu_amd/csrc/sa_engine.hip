@@ -191,6 +191,8 @@ struct Knobs {
     int rows_per_lane = 0;          // SA_ROWS_PER_LANE: force R (1..32)
     int waves_per_group = 0;        // SA_WAVES_PER_GROUP: force W (1..4)
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
+    bool split = false;             // SA_SPLIT=1: score + dir wave per strip for R = 1 global chains
+    int split_w = 2;                // SA_SPLIT_W: strips per split workgroup (1..3)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
@@ -208,6 +210,8 @@ const Knobs &knobs()
         if (const char *e = get("SA_ROWS_PER_LANE")) v.rows_per_lane = std::atoi(e);
         if (const char *e = get("SA_WAVES_PER_GROUP")) v.waves_per_group = std::atoi(e);
         v.no_pair16 = get("SA_NO_PAIR16") != nullptr;
+        v.split = get("SA_SPLIT") != nullptr && std::atoi(get("SA_SPLIT")) != 0;
+        if (const char *e = get("SA_SPLIT_W")) v.split_w = std::min(3, std::max(1, std::atoi(e)));
         if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
         if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
@@ -275,6 +279,7 @@ struct sa_plan {
     int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12, key_rowbits = 21;
     int sk = 0;          // ScoreKind of the fill
     bool chain = false;  // some pair has more than one strip
+    bool split = false;  // R = 1 int8-profile global chains: score + dir wave per strip (sa_split.inc)
     int num_cu = 0;
     std::vector<PairDesc> pairs;
     std::vector<StripDesc> strips;
@@ -731,6 +736,12 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         }
         if (pair) pl->sk = kPair;
     }
+    // the split fill: R = 1 chains with int8 text profiles, global mode
+    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && knobs().split)
+    {
+        pl->split = true;
+        pl->W = knobs().split_w;
+    }
 
     // ---- tables ----
     std::vector<int32_t> &prof = pl->h_prof, &table = pl->h_table;
@@ -933,7 +944,13 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             a.num_groups = (units + W - 1) / W;
             grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
         }
-        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
+        if (pl->split)
+        {
+            // one workgroup per CU (its LDS holds the F rings)
+            grid = std::min(a.num_groups, std::max(1, pl->num_cu));
+            launch_fill_split(a, pl->mode == SA_LOCAL, grid, W, st);
+        }
+        else launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
         HIP_TRY(hipGetLastError());
         if (tlPath)
         {

@@ -61,6 +61,10 @@ constexpr bool kIsArr = SK == kArr || SK == kArr8;
 // Fill launch for strip height R (instantiated in fill_r<R>.hip).
 template <int R>
 void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st);
+// SPLIT fill (R = 1, int8 text profiles, global, strip chains): a score wave and a dir wave per strip,
+// W strips per workgroup (1..3); in fill_r1.hip (sa_split.inc).
+void launch_fill_split(const FillArgs &a, bool local, int grid, int W, hipStream_t st);
+size_t split_fill_lds_bytes(int W);
 #ifndef SA_FILL_R
 extern template void launch_fill_r<1>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
 extern template void launch_fill_r<2>(const FillArgs &, bool, int, int, int, bool, hipStream_t);

@@ -87,7 +87,7 @@ constexpr int kRingMask = kRing - 1;
 #endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
-    defined(SA_EXP_NO_FEED_WAIT)
+    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -107,6 +107,16 @@ struct GroupHdr {
 // lane's sink slot is its ring slot offset: the publish address is one add per body)
 constexpr int kSink = kRing + kWave;
 __host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + ((size_t)(W + 1) * kRing + kSink) * 4; }
+// What a strip's waves see of their workgroup's LDS: the one-wave kernel's GroupHdr, or the split
+// kernel's header and F rings (sa_split.inc)
+struct StripLds {
+    const int *S;   // generic score table (kTable)
+    int *cons;      // cons[w]: columns read from ring[w] (producer backpressure)
+    int nwaves;     // strips of the workgroup (W): the shared sink follows ring W
+    int *frings;    // split: the strips' F rings, else null
+    int *dcons;     // split: dcons[w] = steps whose F values the dir wave of strip w has read
+    int *prog;      // split: prog[w] = steps the score wave of strip w has completed (strips without HN)
+};
 
 // Constant 100 MHz clock, read and waited for in one statement: a compiler-visible s_memrealtime
 // in a slow path can leave its SMEM result "pending" at the join with the fast path, and the
@@ -192,11 +202,13 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // below (HN) that shift's `old` is F[R-1], so lane 63 takes in the previous step's bottom-row value:
 // after U steps lanes 64-U..63 of Q hold the bottom row of steps s0-1 .. s0+U-2, and one full-wave
 // ds_write publishes them (the other lanes write a dummy slot). Steps [QB, QE) of the body.
-template <int R, bool LOCAL, int SK, int KIND, bool HN, int QB, int QE>
+// SPLIT (R = 1): every step's F also goes to this lane's F-ring row at physical slot (s & 127) + 1
+// (sa_split.inc), byte offset frow in LDS; the direction bits are left to the dir wave.
+template <int R, bool LOCAL, int SK, int KIND, bool HN, int QB, int QE, bool SPLIT = false>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Codes<R, SK>::NT],
                                          int (&F)[R], int (&best)[R], int &upPrev, int &Q,
-                                         uint32_t (&acc)[3][Cfg<R>::NW])
+                                         uint32_t (&acc)[3][Cfg<R>::NW], uint32_t frow = 0)
 {
     sfor<QE - QB>([&](auto Qc) {
         constexpr int q = QB + decltype(Qc)::value;
@@ -266,6 +278,7 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 else best[rho] = max(best[rho], key);
             }
             if constexpr (RAMP) Fn = act ? Fn : left;
+            if constexpr (SPLIT) asm volatile("ds_write_b32 %0, %1" ::"v"(frow + ((((uint32_t)s & 127u) + 1u) << 2)), "v"(Fn));
             diag = left;
             up = Fn;
             F[rho] = Fn;
@@ -336,13 +349,51 @@ template <bool LOCAL>
 __device__ __forceinline__ void merge_asm(StepRegs &r);
 #include "sa_fill_steps.inc"
 
+// SPLIT fill (R = 1, int8 text profiles, global; sa_split.inc): each strip has a score wave and a dir
+// wave. The score wave writes every step's F to an LDS F ring: kFRows rows of kFRow dwords per strip,
+// row -1 = the strip's feed (lane 0's `up`) at slot (step & 127), row 1 + k = lane k's F at physical
+// slot (step & 127) + 1 (a body's 16 values are one run: slots up to 128). 132 dwords = 528 bytes = 16
+// times an odd number: the dir wave's lane-strided ds_read_b128 are conflict-free.
+constexpr int kFRow = 132;
+constexpr int kFRows = 65;
+constexpr int kMaxSplitW = 3;  // strips per split workgroup: 2 W + 1 waves (<= 7: 448 threads)
+struct ScoreRegs {
+    int Q, Qn, diag, F;
+    int T[4];
+    uint32_t fra;          // this lane's F-ring row + (s0 & 96) * 4 (the body's writes are offsets)
+    int pfaddr, pf;        // HP: as StepRegs
+    int pubaddr, pubtag, ctag, msb;
+    uint64_t bad;
+    uint32_t dcaddr;       // DC: LDS address of the dir wave's consumption word
+    int dcv;               // DC: its value, read during the block
+};
+struct DirRegs {
+    int O[16], U[16];      // O[i] = F_{s0+i-1} (i >= 1), U[i] = the lane above's F_{s0+i-1} / the feed
+    int oc, ex;            // F_{s0-1} (carried), F_{s0+15}
+    int X[8], Y[8];        // direction differences, one byte per step (as StepRegs)
+    int mk[8];
+    uint32_t acc0, acc1;
+};
+template <bool HN, bool HP, int HALF, bool DC>
+__device__ __forceinline__ void score_asm(ScoreRegs &r);
+template <int HALF>
+__device__ __forceinline__ void dir_asm(DirRegs &r);
+#if SA_FILL_R == 1
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_SPLIT_INC)
+#include SA_EXP_SPLIT_INC  // tools/gen_split_asm.py variants (timing ablations)
+#else
+#include "sa_split_steps.inc"
+#endif
+#endif
+
 // One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
 // kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
-template <int R, bool LOCAL, int SK, bool HP, bool HN>
-__device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, lds_int *rings, int idx, int w, int lane)
+template <int R, bool LOCAL, int SK, bool HP, bool HN, bool SPLIT = false>
+__device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
+    static_assert(!SPLIT || (R == 1 && SK == kArr8 && !LOCAL), "the split fill is R = 1, int8 profiles, global");
     constexpr int U = Cfg<R>::U;
     constexpr int NT = Codes<R, SK>::NT;
     // Descriptors come in through vector loads (the kernel stores to global memory, so the compiler
@@ -386,11 +437,11 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         coff = (uint32_t)((kPad - lane) * 4);
     lds_int *rin = (lds_int *)(rings + w * kRing);
     lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
-    lds_int *consIn = (lds_int *)&H.cons[w];
-    lds_int *consOut = (lds_int *)&H.cons[w + 1];
+    lds_int *consIn = (lds_int *)&L.cons[w];
+    lds_int *consOut = (lds_int *)&L.cons[w + 1];
     // publish target of this lane at ring offset 0: lanes 64-U..63 their column's slot, the others
     // the sink (rings + (W+1) * kRing, shared by the waves: its contents are never read)
-    lds_int *pubBase = lane >= kWave - U ? rout + (lane - (kWave - U)) : rings + (H.nwaves + 1) * kRing + lane;
+    lds_int *pubBase = lane >= kWave - U ? rout + (lane - (kWave - U)) : rings + (L.nwaves + 1) * kRing + lane;
     // the strip's direction chunks (uniform base) and this lane's byte offset in a chunk
     uint32_t *mbase = a.masks + sd.mask_off * 4;
     const uint32_t moff = (uint32_t)(lane * Cfg<R>::LW * 4);
@@ -580,6 +631,44 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
     };
     int msbv;  // one VGPR for the strip (the compiler would rematerialize a literal per body)
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
+    // SPLIT: this lane's F-ring row, where its Q lane goes (lanes 0..15: the feed row -1; others: the
+    // sink), the dir wave's consumption word, and (strips without HN) the progress word
+    uint32_t frowOff = 0, feedOff = 0, progOff = 0;
+    int dKnown = 0;  // steps the dir wave is known to have consumed
+    uint32_t dWaits = 0;  // timeline: bodies that waited for the dir wave
+    if constexpr (SPLIT)
+    {
+        int *fr = L.frings + w * kFRows * kFRow;
+        frowOff = lds_off((lds_int *)(fr + (1 + lane) * kFRow));
+        const lds_int *sink = rings + (L.nwaves + 1) * kRing;
+        feedOff = lane < U ? lds_off((lds_int *)(fr + lane)) : lds_off(sink + lane);
+        progOff = lane == 0 ? lds_off((lds_int *)&L.prog[w]) : lds_off(sink + lane);
+    }
+    // F ring backpressure: a body at s0 overwrites the slots of steps s0 - 128 .. s0 - 113, which
+    // the dir wave has read once it has consumed s0 - 112
+    auto dcons_wait = [&](int need) __attribute__((always_inline)) {
+        if constexpr (SPLIT)
+        {
+            const uint64_t t0 = now_ticks();
+            ++dWaits;
+            for (uint32_t spin = 1;; ++spin)
+            {
+                dKnown = uniform(ds_read_sync((lds_int *)&L.dcons[w]));
+                if (dKnown >= need) break;
+                __builtin_amdgcn_s_sleep(1);
+                if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+            }
+        }
+    };
+    auto split_pre = [&](int s0) __attribute__((always_inline)) {
+        // the feed (Q lanes 0..15) -> row -1, slot (s0 & 127) + lane: the dir wave's lane-0 `up`
+        if constexpr (SPLIT) asm volatile("ds_write_b32 %0, %1" ::"v"(feedOff + (uint32_t)((s0 & 127) * 4)), "v"(Q));
+    };
+    auto split_post = [&](int s0) __attribute__((always_inline)) {
+        // strips without HN tell their dir wave through the progress word (with HN it polls the
+        // published bottom row)
+        if constexpr (SPLIT && !HN) asm volatile("ds_write_b32 %0, %1" ::"v"(progOff), "v"(s0 + U));
+    };
     // the asm bodies' direction-difference bytes (kept across the two bodies of a plane word) and the
     // merge masks 0x80808080 >> g (opaque: built once per strip, not rematerialized per word)
     int dX[8], dY[8], dZ[8], mkv[8], mzv[4];
@@ -625,7 +714,44 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         }
 #endif
         load_codes(s0 + kAhead * U, Tn);
-        if constexpr (kAsm && KIND == kSteady)
+        if constexpr (SPLIT && kAsm && KIND == kSteady)
+        {
+            constexpr int HALF = POS & 1;
+            constexpr bool DC = HALF == 0;  // one consumption read per body pair
+            ScoreRegs r;
+            split_pre(s0);
+            r.Q = Q;
+            r.diag = upPrev;
+            r.F = F[0];
+            sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
+            r.fra = frowOff + (uint32_t)((s0 & 96) * 4);
+            r.pfaddr = HP ? (int)(rinLaneOff + 4u * (uint32_t)ring_slot(s1 + 1)) : 0;
+            r.ctag = ring_tag_raw(s1 + 1);
+            r.msb = msbv;
+            if constexpr (POS == 0) pub_wait(s0 + 3 * U);
+            else if constexpr (POS == 2) pub_wait(s0 + U);
+            r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
+            r.pubtag = ring_tag_raw(s0 - 63);
+            r.dcaddr = lds_off((lds_int *)&L.dcons[w]);
+            score_asm<HN, HP, HALF, DC>(r);
+            if constexpr (HP)
+            {
+                pfVal = r.pf;
+                pfBad = r.bad;
+                pfTagged = true;
+            }
+            Q = r.Q;
+            upPrev = r.diag;
+            F[0] = r.F;
+            split_post(s0);
+            if constexpr (DC)
+            {
+                // the next pair (s0 + 32, s0 + 48) needs the dir wave at s0 + 48 - 112
+                dKnown = uniform(r.dcv);
+                if (__builtin_expect(s0 - 64 > dKnown, 0)) dcons_wait(s0 - 64);
+            }
+        }
+        else if constexpr (kAsm && KIND == kSteady)
         {
             static_assert(U == 16 && NT == 4, "sa_fill_steps.inc is generated for these");
             StepRegs r;
@@ -684,16 +810,22 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         }
         else
         {
-            run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+            if constexpr (SPLIT)
+            {
+                if (s0 - 112 > dKnown) dcons_wait(s0 - 112);
+                split_pre(s0);
+            }
+            run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead, SPLIT>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc, frowOff);
             prefetch(s1);
-            run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(H.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
+            run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U, SPLIT>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc, frowOff);
             // R = 1: a body fills one interleaved word; the chunk's first word waits in acc[1][0]
             if constexpr (R == 1 && !second::value) acc[1][0] = acc[0][0];
+            split_post(s0);
         }
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STORE)
         if constexpr (false)  // timing ablation: no direction planes are written
 #else
-        if constexpr (Cfg<R>::BPC == 1 || second::value)
+        if constexpr (!SPLIT && (Cfg<R>::BPC == 1 || second::value))
 #endif
         {
             const int chunk = (s1 * R) / Cfg<R>::CS - 1;
@@ -812,6 +944,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, GroupHdr &H, ld
         tl[41] = dbgFeedSpinsSteady;
 #endif
         tl[5] = __builtin_amdgcn_s_memtime();
+        if constexpr (SPLIT) tl[45] = dWaits;
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
         tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
                 (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
@@ -1035,7 +1168,7 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
-__device__ __forceinline__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int *rings, int grp, int W, int lane)
+__device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
     const int last = min(first + W, a.num_strips) - 1;
@@ -1046,9 +1179,9 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, GroupHdr &H, lds_int 
     if (nIn == 0 && nOut == 0) return;
     const int wl = last - first + 1;  // ring fed by the last strip
     lds_int *r0 = (lds_int *)rings;
-    lds_int *cons0 = (lds_int *)&H.cons[0];
+    lds_int *cons0 = (lds_int *)&cons[0];
     lds_int *rl = (lds_int *)(rings + wl * kRing);
-    lds_int *consL = (lds_int *)&H.cons[wl];
+    lds_int *consL = (lds_int *)&cons[wl];
     const uint64_t *bin = a.bnd + sf.bnd_in;
     uint64_t *bout = a.bnd + sl.bnd_out;
     int copied = 0, drained = 0;
@@ -1164,7 +1297,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         if (grp >= a.num_groups) break;
         if (CHAIN && w == W)
         {
-            io_wave(a, H, rings, grp, W, lane);
+            io_wave(a, H.cons, rings, grp, W, lane);
         }
         else
         {
@@ -1175,17 +1308,18 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
                 // variant is instantiated, which keeps the register count of the batch kernel down)
                 const int f = uniform(a.strips[idx].flags) & (kHasPrev | kHasNext);
+                const StripLds L{H.S, H.cons, H.nwaves, nullptr, nullptr, nullptr};
                 if constexpr (CHAIN)
                 {
-                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, H, rings, idx, w, lane);
-                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, H, rings, idx, w, lane);
-                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, H, rings, idx, w, lane);
-                    else process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
+                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
+                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, L, rings, idx, w, lane);
+                    else process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
                 }
                 else
                 {
                     (void)f;
-                    process_strip<R, LOCAL, SK, false, false>(a, H, rings, idx, w, lane);
+                    process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
                 }
             }
         }
@@ -1252,5 +1386,9 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
 }
 
 template void launch_fill_r<SA_FILL_R>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+
+#if SA_FILL_R == 1
+#include "sa_split.inc"
+#endif
 
 }  // namespace sa

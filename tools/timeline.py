@@ -74,6 +74,10 @@ def main():
     clk = (tl[:, 5].astype(np.int64) - tl[:, 4].astype(np.int64))
     mhz = clk / np.maximum(1, (end - fed)) * 100.0  # s_memtime ticks per s_memrealtime (100 MHz) tick
     W = int(os.environ.get("SA_WAVES_PER_GROUP", "4"))
+    # the split fill (R = 1 global int8-profile chains) runs SA_SPLIT_W strips per workgroup
+    split = args.mode == 0 and args.R == 1 and args.m > 64 and os.environ.get("SA_SPLIT", "0") != "0"
+    if split:
+        W = int(os.environ.get("SA_SPLIT_W", "2"))
     k = np.arange(1, len(fed))
     cross = (k % W) == 0
     rec = {
@@ -105,6 +109,17 @@ def main():
         "ns_per_step_by_wave_in_group": [round(float(step_ns[w::W].mean()), 2) for w in range(W)],
         "ns_per_step_by_simd": [round(float(step_ns[((hw >> 4) & 3) == q].mean()), 2) if (((hw >> 4) & 3) == q).any() else None for q in range(4)],
     }
+    if split:
+        # dir waves (timeline words 42..46): how far each ends behind its score wave, how often it
+        # found its body unfinished, how often the score wave waited for it, and where it ran
+        dend = tl[:, 43].astype(np.int64)
+        dhw = (tl[:, 46] & 0xffffffff).astype(np.int64)
+        rec["split"] = {
+            "dir_end_behind_score_ns_mean": round(float(((dend - end) * 10.0).mean()), 1),
+            "dir_waiting_polls_mean": round(float(tl[:, 44].astype(np.int64).mean()), 1),
+            "score_waits_for_dir_mean": round(float(tl[:, 45].astype(np.int64).mean()), 2),
+            "dir_simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in dhw[:8]],
+        }
     prog = tl[:, 6:16].astype(np.int64)
     iop = tl[:, 16:26].astype(np.int64)
     if prog[:, 1].any():
