@@ -87,12 +87,13 @@ constexpr int kRingMask = kRing - 1;
 #endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
-    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR)
+    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
 #define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
 #endif
+constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer resource, dword 3 (no format, no swizzle)
 constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
 
 struct GroupHdr {
@@ -476,6 +477,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     // touch of a code line misses L2); taller strips double-buffer across the two bodies of a pair
     constexpr int kAhead = R != 1 ? 1 : kCodeAhead;
     int TA[NT], TB[NT], TC[NT], TD[NT];
+    // R = 1: the text codes and the direction chunks go through buffer resources (SGPR base, the
+    // lane's constant 32-bit offset in a VGPR, the step-dependent part in an SGPR soffset), so a body's
+    // load and a chunk's store need no VALU address arithmetic and no 64-bit adds
+    constexpr bool kBuf = R == 1;
+    const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(cbase), 0, 0x7fffffff, kBufRsrcWord3);
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(mbase, 0, 0x7ffffff0, kBufRsrcWord3);
     auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_CODES_CONST)
@@ -483,6 +490,20 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 #else
         const uint32_t off = coff + (uint32_t)(SK == kArr8 ? s0 : s0 * 4);
 #endif
+        if constexpr (kBuf)
+        {
+            const int soff = SK == kArr8 ? s0 : s0 * 4;
+            sfor<NT / 4>([&](auto Qc) {
+                constexpr int q = decltype(Qc)::value * 4;
+                const i32x4u v = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff, soff + q * 4, 0);
+                dst[q] = v.x;
+                dst[q + 1] = v.y;
+                dst[q + 2] = v.z;
+                dst[q + 3] = v.w;
+            });
+            (void)off;
+            return;
+        }
         sfor<NT / 4>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value * 4;
             const i32x4u v = *(const i32x4u *)(cbase + off + q * 4);
@@ -506,7 +527,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     int pfVal = 0;
     bool pfTagged = false;  // pfVal already XORed with its tag by the asm body, bad lanes in pfBad
     uint64_t pfBad = 0;
-    int consDone = 0;    // last consumption word written
     // address of this lane's feed slot for the body starting at step base (column base+1+lane): the
     // body's 16 slots are one aligned run (ring_slot), so the wrap is applied to the uniform part only
     // (lanes >= U read past it, into the next ring or the sink: their values are never used)
@@ -587,14 +607,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         }
     };
     // consumption word for the strip above (its backpressure), at most every kConsEvery columns
+    // (once per loop trip: every lane writes, lane 0 the word and the others into the sink, so the
+    // write is one instruction instead of an exec-masked branch; asm: no LDS operation of the
+    // compiler's may stay in flight into the next body)
+    const uint32_t consAddr = lane == 0 ? lds_off(consIn) : lds_off(rings + (L.nwaves + 1) * kRing + lane);
     auto consumed = [&](int upto) __attribute__((always_inline)) {
-        if constexpr (HP)
-            if (upto - consDone >= kConsEvery)
-            {
-                consDone = upto;
-                // (asm: no LDS operation of the compiler's may stay in flight into the next body)
-                if (lane == 0) ds_write_async(consIn, upto);
-            }
+        if constexpr (HP) asm volatile("ds_write_b32 %0, %1" ::"v"(consAddr), "v"(upto));
     };
     // lanes 64-U..63 of Q hold the bottom row of columns s0-63 .. s0-64+U: one ds_write_b32 by every
     // lane (the others into the sink), tagged, after making sure the consumer has read the slots'
@@ -699,6 +717,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     // pos: the body's place in its loop trip (0..3 in quads, 0..1 in pairs): odd bodies store the
     // direction chunk (two bodies per chunk for R = 1), the trip's last one writes the consumption word.
     // full: the next body's feed is known to be fully published (feed()) and s1 < nSteps.
+    // the loop trip's feed-slot byte offset 4 (s0q + U + 64) (the trip's bodies add 4 U POS and wrap),
+    // opaque so the compiler computes it once per trip instead of per body from the step
+    uint32_t quadPf = 0;
+    auto set_quad = [&](int s0q) __attribute__((always_inline)) {
+        quadPf = 4u * (uint32_t)s0q + 4u * (U + 64);
+        asm volatile("" : "+s"(quadPf));
+    };
     auto body = [&](auto kind, auto pos, auto full, int s0, int (&T)[NT], int (&Tn)[NT]) __attribute__((always_inline)) {
         constexpr int KIND = decltype(kind)::value;
         constexpr int POS = decltype(pos)::value;
@@ -768,7 +793,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
             r.g = g;
             r.kb = kb;
-            r.pfaddr = HP ? (int)(rinLaneOff + 4u * (uint32_t)ring_slot(s1 + 1)) : 0;
+            // 4 * ring_slot(s1 + 1) = (4 s0 + 4 (U + 64)) mod 8 KiB, from the loop trip's base (quadPf)
+            r.pfaddr = HP ? (int)(rinLaneOff + ((quadPf + 4u * U * POS) & (4u * kRingMask))) : 0;
             r.ctag = ring_tag_raw(s1 + 1);
             r.msb = msbv;
             // the block ends with the publish write (HN); one backpressure check covers the bodies up
@@ -798,9 +824,15 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
                 // the chunk's second body: its bits into the two interleaved words for the store below
                 sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
                 if constexpr (LOCAL) sfor<4>([&](auto Tc) { r.mz[decltype(Tc)::value] = mzv[decltype(Tc)::value]; });
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_MERGE)
+                // timing ablation: the chunk's words are two raw difference registers (results wrong)
+                acc[1][0] = (uint32_t)r.X[0] ^ (uint32_t)r.X[5];
+                acc[0][0] = (uint32_t)r.Y[0] ^ (uint32_t)r.Y[5];
+#else
                 merge_asm<LOCAL>(r);
                 acc[1][0] = r.acc0;
                 acc[0][0] = r.acc1;
+#endif
             }
             if constexpr (LOCAL)
             {
@@ -828,8 +860,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         if constexpr (!SPLIT && (Cfg<R>::BPC == 1 || second::value))
 #endif
         {
-            const int chunk = (s1 * R) / Cfg<R>::CS - 1;
-            store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);
+            const int chunk = (int)((uint32_t)(s1 * R) / Cfg<R>::CS) - 1;
+            if constexpr (kBuf)
+                // R = 1: the chunk's two interleaved words (store_chunk), soffset = the chunk's byte offset
+                __builtin_amdgcn_raw_buffer_store_b64(u32x2{acc[1][0], acc[0][0]}, mrsrc, moff, chunk * (kWave * Cfg<R>::LW * 4), 0);
+            else
+                store_chunk<R, LOCAL>(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(mbase + (size_t)chunk * (kWave * Cfg<R>::LW)) + moff), acc);
         }
         if constexpr (LOCAL)
         {
@@ -877,6 +913,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         auto phase = [&](auto kind, auto full, int end) __attribute__((always_inline)) {
             for (; s0 + 2 * U < end; s0 += 4 * U)
             {
+                set_quad(s0);
                 body(kind, P0{}, full, s0, TA, TC);
                 body(kind, P1{}, full, s0 + U, TB, TD);
                 body(kind, P2{}, full, s0 + 2 * U, TC, TA);
@@ -884,6 +921,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             }
             if (s0 < end)
             {
+                set_quad(s0 - 2 * U);
                 body(kind, P2{}, full, s0, TA, TC);
                 body(kind, P3{}, full, s0 + U, TB, TD);
                 s0 += 2 * U;
