@@ -193,6 +193,8 @@ struct Knobs {
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
     bool split = false;             // SA_SPLIT=1: score + dir wave per strip for R = 1 global chains
     int split_w = 2;                // SA_SPLIT_W: strips per split workgroup (1..3)
+    bool dual = false;              // SA_DUAL=1: score waves + direction tasks (sa_fill.hip, DUAL)
+    int dual_seg = 1024;            // SA_DUAL_SEG: steps per direction task (a multiple of 64)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
@@ -212,6 +214,14 @@ const Knobs &knobs()
         v.no_pair16 = get("SA_NO_PAIR16") != nullptr;
         v.split = get("SA_SPLIT") != nullptr && std::atoi(get("SA_SPLIT")) != 0;
         if (const char *e = get("SA_SPLIT_W")) v.split_w = std::min(3, std::max(1, std::atoi(e)));
+        if (const char *e = get("SA_DUAL")) v.dual = std::atoi(e) != 0;
+        if (const char *e = get("SA_DUAL_SEG"))
+        {
+            // a power of two, at least 64 (the score waves test segment starts with a mask)
+            int sg = 64;
+            while (sg * 2 <= std::atoi(e)) sg *= 2;
+            v.dual_seg = sg;
+        }
         if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
         if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
@@ -280,6 +290,11 @@ struct sa_plan {
     int sk = 0;          // ScoreKind of the fill
     bool chain = false;  // some pair has more than one strip
     bool split = false;  // R = 1 int8-profile global chains: score + dir wave per strip (sa_split.inc)
+    bool dual = false;   // R = 1 int8-profile global chains: score waves + direction tasks (sa_fill.hip)
+    int seg_len = 0, seg_stride = 0;
+    std::vector<int32_t> h_tasks;  // dual: {strip, segment} pairs in the order direction waves take them
+    int32_t *d_tasks = nullptr;
+    uint64_t *d_snap = nullptr;
     int num_cu = 0;
     std::vector<PairDesc> pairs;
     std::vector<StripDesc> strips;
@@ -368,7 +383,7 @@ void free_plan(sa_plan *p)
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
-                    p->d_out_pattern, p->d_results};
+                    p->d_out_pattern, p->d_results, p->d_tasks, p->d_snap};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -742,6 +757,40 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         pl->split = true;
         pl->W = knobs().split_w;
     }
+    // the dual fill: the same chains, when the strip groups leave at least half of the CUs to the
+    // direction waves (one workgroup per CU, so no CU runs both)
+    const int64_t groups = ((int64_t)pl->strips.size() + pl->W - 1) / pl->W;
+    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && !pl->split && knobs().dual &&
+        groups <= pl->num_cu / 2)
+    {
+        pl->dual = true;
+        pl->seg_len = knobs().dual_seg;
+        int jmax = 1;
+        for (const StripDesc &sd : pl->strips) jmax = std::max(jmax, (sd.nsteps + pl->seg_len - 1) / pl->seg_len);
+        pl->seg_stride = jmax;
+        // tasks in the order their data appears: strip k (of its pair) reaches segment j after about
+        // k hand-off lags (~112 steps) plus (j + 1) segments, so the key is k + D (j + 1), D = seg / 112
+        const int D = std::max(1, pl->seg_len / 112);
+        int64_t dmax = 0;
+        for (const PairDesc &d : pl->pairs)
+            if (d.num_strips > 0)
+                dmax = std::max<int64_t>(dmax, d.num_strips - 1 + (int64_t)D * ((pl->strips[d.first_strip].nsteps + pl->seg_len - 1) / pl->seg_len));
+        for (int64_t key = 0; key <= dmax; ++key)
+            for (const PairDesc &d : pl->pairs)
+            {
+                if (d.num_strips == 0) continue;
+                const int J = (pl->strips[d.first_strip].nsteps + pl->seg_len - 1) / pl->seg_len;
+                for (int jj = 0; jj < J; ++jj)
+                {
+                    const int64_t k = key - (int64_t)D * (jj + 1);
+                    if (k >= 0 && k < d.num_strips)
+                    {
+                        pl->h_tasks.push_back(d.first_strip + (int32_t)k);
+                        pl->h_tasks.push_back(jj);
+                    }
+                }
+            }
+    }
 
     // ---- tables ----
     std::vector<int32_t> &prof = pl->h_prof, &table = pl->h_table;
@@ -768,6 +817,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_strips, sizeof(StripDesc) * nstr},
         {(void **)&pl->d_prof, sizeof(int32_t) * 4},
         {(void **)&pl->d_table, sizeof(int32_t) * A * A},
+        {(void **)&pl->d_tasks, sizeof(int32_t) * pl->h_tasks.size()},
         {(void **)&pl->d_ws_text, in ? inN + 16 : 0},
         {(void **)&pl->d_ws_pattern, in ? inM + 16 : 0},
         {(void **)&pl->d_ctrl, sizeof(Control)},
@@ -777,6 +827,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_codes, codeB},
         // (+8 KiB: the traceback's plane prefetch may read a few chunks past a strip)
         {(void **)&pl->d_masks, pl->bytes_masks + 8192},
+        {(void **)&pl->d_snap, pl->dual ? sizeof(uint64_t) * 2 * kWave * pl->strips.size() * pl->seg_stride : 0},
         {(void **)&pl->d_bnd, ws ? 0 : bndB},  // (workspace plans: the context's granule buffer)
         {(void **)&pl->d_best, bestB},
         {(void **)&pl->d_score, sizeof(int32_t) * npp},
@@ -819,6 +870,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         put(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size());
         put(pl->d_prof, prof.data(), sizeof(int32_t) * 4);
         put(pl->d_table, table.data(), sizeof(int32_t) * A * A);
+        put(pl->d_tasks, pl->h_tasks.data(), sizeof(int32_t) * pl->h_tasks.size());
         put(pl->d_ws_text, in->text, inN);
         put(pl->d_ws_pattern, in->pattern, inM);
         std::memset(h + ((char *)pl->d_ctrl - pl->d_up), 0, sizeof(Control));
@@ -845,6 +897,9 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemcpyAsync(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(pl->d_bnd, 0, bndB, st) == hipSuccess &&
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
+    if (okc && pl->dual)
+        okc = hipMemcpyAsync(pl->d_tasks, pl->h_tasks.data(), sizeof(int32_t) * pl->h_tasks.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemsetAsync(pl->d_snap, 0, sizeof(uint64_t) * 2 * kWave * pl->strips.size() * pl->seg_stride, st) == hipSuccess;
     // a plan of its own is complete when sa_plan_create returns (callers fill on other streams)
     if (okc) okc = hipStreamSynchronize(st) == hipSuccess;
     if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
@@ -921,6 +976,13 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.timeout_ticks = (uint64_t)(knobs().handoff_timeout_s * 1e8);
         a.io_sleep = knobs().io_sleep;
         a.chain_lds = knobs().chain_lds_kb * 1024;
+        a.dual = 0;
+        a.score_wgs = 0;
+        a.seg_len = pl->seg_len;
+        a.seg_stride = pl->seg_stride;
+        a.num_dir_tasks = (int32_t)(pl->h_tasks.size() / 2);
+        a.dir_tasks = pl->d_tasks;
+        a.snap = pl->d_snap;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;
@@ -943,6 +1005,16 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const int units = ns / 2;
             a.num_groups = (units + W - 1) / W;
             grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
+        }
+        if (pl->dual)
+        {
+            // strip groups on the first workgroups, direction workers on the rest, one workgroup per
+            // CU (the LDS request is above half a CU's), so no CU runs a score wave and a direction
+            // wave side by side
+            a.dual = 1;
+            a.score_wgs = a.num_groups;
+            a.chain_lds = std::max(a.chain_lds, 96 * 1024);
+            grid = std::max(a.num_groups + 1, pl->num_cu);
         }
         if (pl->split)
         {

@@ -34,6 +34,16 @@ struct FillArgs {
     int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
     int32_t chain_lds;          // chain launches: dynamic LDS bytes (>= group_lds_bytes(W); more
                                 // than half a CU's LDS keeps one workgroup per CU)
+    // DUAL fill (R = 1 int8-profile global chains, sa_fill.hip): score waves run the recurrence
+    // alone, publish every bottom row to bnd and snapshot their state every seg_len steps; direction
+    // waves on the other CUs recompute each (strip, segment) from that and write the planes
+    int32_t dual;               // 0: one-wave fill
+    int32_t score_wgs;          // dual: workgroups [0, score_wgs) take strip groups, the rest direction tasks
+    int32_t seg_len;            // dual: steps per segment (a multiple of 64)
+    int32_t seg_stride;         // dual: snapshot entries per strip
+    int32_t num_dir_tasks;
+    const int32_t *dir_tasks;   // dual: {strip, segment} in the order direction waves take them
+    uint64_t *snap;             // dual: per (strip, segment) {value, epoch} of F and diag, 64 lanes each
 };
 
 constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip (words 6..35: experiment progress stamps)

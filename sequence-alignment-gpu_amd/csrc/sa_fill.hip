@@ -87,21 +87,23 @@ constexpr int kRingMask = kRing - 1;
 #endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
-    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE)
+    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
 #define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
 #endif
 constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer resource, dword 3 (no format, no swizzle)
+constexpr int kAuxSc1 = 16;                // buffer access cache policy: sc1 (agent-coherent, as the granules)
 constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
     int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
+    int drain[kMaxWaves + 1];      // dual: drain[w]: columns of ring[w] the I/O wave has copied to granules
     int group;                     // group index taken from the queue
     int nwaves;                    // compute waves of the workgroup (W)
-    int pad[1];
 };
 // chain workgroup LDS: header, W + 1 rings, then one shared sink that the lanes carrying no
 // bottom-row value write into when their wave publishes (a ring's size plus a wave, so that a
@@ -117,6 +119,7 @@ struct StripLds {
     int *frings;    // split: the strips' F rings, else null
     int *dcons;     // split: dcons[w] = steps whose F values the dir wave of strip w has read
     int *prog;      // split: prog[w] = steps the score wave of strip w has completed (strips without HN)
+    int *drain;     // dual: drain[w] = columns of ring[w] the I/O wave has copied to granules
 };
 
 // Constant 100 MHz clock, read and waited for in one statement: a compiler-visible s_memrealtime
@@ -348,7 +351,13 @@ template <bool LOCAL, bool HN, bool HP, int HALF>
 __device__ __forceinline__ void steps_asm(StepRegs &r);
 template <bool LOCAL>
 __device__ __forceinline__ void merge_asm(StepRegs &r);
+template <bool HN, bool HP>
+__device__ __forceinline__ void rec_steps_asm(StepRegs &r);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_FILL_INC)
+#include SA_EXP_FILL_INC  // tools/gen_fill_asm.py variants (timing ablations)
+#else
 #include "sa_fill_steps.inc"
+#endif
 
 // SPLIT fill (R = 1, int8 text profiles, global; sa_split.inc): each strip has a score wave and a dir
 // wave. The score wave writes every step's F to an LDS F ring: kFRows rows of kFRow dwords per strip,
@@ -391,10 +400,11 @@ __device__ __forceinline__ void dir_asm(DirRegs &r);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
 // kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
-template <int R, bool LOCAL, int SK, bool HP, bool HN, bool SPLIT = false>
+template <int R, bool LOCAL, int SK, bool HP, bool HN, bool SPLIT = false, bool DUALS = false>
 __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     static_assert(!SPLIT || (R == 1 && SK == kArr8 && !LOCAL), "the split fill is R = 1, int8 profiles, global");
+    static_assert(!DUALS || (R == 1 && SK == kArr8 && !LOCAL && !SPLIT), "the dual fill is R = 1, int8 profiles, global");
     constexpr int U = Cfg<R>::U;
     constexpr int NT = Codes<R, SK>::NT;
     // Descriptors come in through vector loads (the kernel stores to global memory, so the compiler
@@ -633,12 +643,26 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
                     ++dbgPubSpins;
 #endif
                     consKnown = uniform(lds_ld(consOut));
+                    // dual: the I/O wave copies this ring to granules too and must have read a slot
+                    if constexpr (DUALS) consKnown = min(consKnown, uniform(lds_ld((lds_int *)&L.drain[w + 1])));
                     if (cLast - kRing <= consKnown) break;
                     __builtin_amdgcn_s_sleep(1);
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
                 }
             }
         }
+    };
+    // DUAL score wave: every seg_len steps its state (F of the step before, diag) goes to the strip's
+    // snapshot entry (its bottom row reaches the granules through the I/O wave, io_wave)
+    const uint32_t epochv = a.epoch;
+    auto snapshot = [&](int s0, int f, int dg) __attribute__((always_inline)) {
+        if constexpr (DUALS)
+            if (s0 > 0 && (s0 & (a.seg_len - 1)) == 0)  // (seg_len: a power of two)
+            {
+                uint64_t *e = a.snap + ((size_t)idx * a.seg_stride + (uint32_t)s0 / (uint32_t)a.seg_len) * (2 * kWave) + lane;
+                __hip_atomic_store(e, ((uint64_t)epochv << 32) | (uint32_t)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(e + kWave, ((uint64_t)epochv << 32) | (uint32_t)dg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
     };
     auto publish = [&](int s0) __attribute__((always_inline)) {
         if constexpr (HN)
@@ -739,6 +763,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         }
 #endif
         load_codes(s0 + kAhead * U, Tn);
+        snapshot(s0, F[0], upPrev);
         if constexpr (SPLIT && kAsm && KIND == kSteady)
         {
             constexpr int HALF = POS & 1;
@@ -783,12 +808,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             r.Q = Q;
             r.diag = upPrev;
             r.F = F[0];
-            sfor<8>([&](auto Gc) {
-                constexpr int g = decltype(Gc)::value;
-                r.X[g] = dX[g];
-                r.Y[g] = dY[g];
-                if constexpr (LOCAL) r.Z[g] = dZ[g];
-            });
+            if constexpr (!DUALS)
+                sfor<8>([&](auto Gc) {
+                    constexpr int g = decltype(Gc)::value;
+                    r.X[g] = dX[g];
+                    r.Y[g] = dY[g];
+                    if constexpr (LOCAL) r.Z[g] = dZ[g];
+                });
             r.bm = -16;  // below every (H << kb) - q
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
             r.g = g;
@@ -803,7 +829,8 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             else if constexpr (POS == 2) pub_wait(s0 + U);
             r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
             r.pubtag = ring_tag_raw(s0 - 63);
-            steps_asm<LOCAL, HN, HP, POS & 1>(r);  // with HP: reads the next body's feed after step 12
+            if constexpr (DUALS) rec_steps_asm<HN, HP>(r);  // the recurrence alone (direction waves)
+            else steps_asm<LOCAL, HN, HP, POS & 1>(r);  // with HP: reads the next body's feed after step 12
             if constexpr (HP)
             {
                 pfVal = r.pf;
@@ -813,13 +840,14 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             Q = r.Q;
             upPrev = r.diag;
             F[0] = r.F;
-            sfor<8>([&](auto Gc) {
-                constexpr int g = decltype(Gc)::value;
-                dX[g] = r.X[g];
-                dY[g] = r.Y[g];
-                if constexpr (LOCAL) dZ[g] = r.Z[g];
-            });
-            if constexpr ((POS & 1) == 1)
+            if constexpr (!DUALS)
+                sfor<8>([&](auto Gc) {
+                    constexpr int g = decltype(Gc)::value;
+                    dX[g] = r.X[g];
+                    dY[g] = r.Y[g];
+                    if constexpr (LOCAL) dZ[g] = r.Z[g];
+                });
+            if constexpr ((POS & 1) == 1 && !DUALS)
             {
                 // the chunk's second body: its bits into the two interleaved words for the store below
                 sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
@@ -857,7 +885,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STORE)
         if constexpr (false)  // timing ablation: no direction planes are written
 #else
-        if constexpr (!SPLIT && (Cfg<R>::BPC == 1 || second::value))
+        if constexpr (!SPLIT && !DUALS && (Cfg<R>::BPC == 1 || second::value))
 #endif
         {
             const int chunk = (int)((uint32_t)(s1 * R) / Cfg<R>::CS) - 1;
@@ -1206,7 +1234,7 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
-__device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, lds_int *rings, int grp, int W, int lane)
+__device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain, lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
     const int last = min(first + W, a.num_strips) - 1;
@@ -1214,7 +1242,6 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, lds_int *r
     const StripDesc sl = a.strips[last];
     const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
     const int nOut = (sl.flags & kHasNext) ? (int)a.pairs[sl.pair].text_len : 0;
-    if (nIn == 0 && nOut == 0) return;
     const int wl = last - first + 1;  // ring fed by the last strip
     lds_int *r0 = (lds_int *)rings;
     lds_int *cons0 = (lds_int *)&cons[0];
@@ -1226,10 +1253,55 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, lds_int *r
     // slots of columns -63..0 are never copied in: give them their lap-0 tag, or the zeroed entries
     // would pass for lap-1 columns 1985..2048 (a compute-wave producer publishes from column -63)
     if (nIn > 0) lds_st(r0 + ring_slot(lane - 63), ring_tag(lane - 63));
+    // dual: rings 1 .. wl-1 (fed by strips first .. last-1) go to those strips' granules as well, the
+    // direction waves' feed (the compute waves publish into LDS only)
+    int dr[kMaxWaves - 1], drN[kMaxWaves - 1];
+    uint64_t *drOut[kMaxWaves - 1];
+    bool drPending = false;
+    sfor<kMaxWaves - 1>([&](auto Rc) {
+        constexpr int r = decltype(Rc)::value;  // ring r + 1, strip first + r
+        dr[r] = 0;
+        drN[r] = 0;
+        drOut[r] = a.bnd;
+        if (a.dual && r + 1 < wl)
+        {
+            const StripDesc sr = a.strips[first + r];
+            if (uniform(sr.flags) & kHasNext)
+            {
+                drN[r] = (int)uniform64(a.pairs[uniform(sr.pair)].text_len);
+                drOut[r] = a.bnd + uniform64(sr.bnd_out);
+                drPending = true;
+            }
+        }
+    });
+    if (nIn == 0 && nOut == 0 && !drPending) return;
     uint64_t t0 = now_ticks();
-    for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
+    for (uint32_t spin = 1; copied < nIn || drained < nOut || drPending; ++spin)
     {
         bool moved = false;
+        if (drPending)
+        {
+            drPending = false;
+            sfor<kMaxWaves - 1>([&](auto Rc) {
+                constexpr int r = decltype(Rc)::value;
+                // (up to 4 x 64 columns per pass: the score waves outrun one window per poll round trip)
+                for (int rep = 0; rep < 4 && dr[r] < drN[r]; ++rep)
+                {
+                    const int c = dr[r] + lane + 1;
+                    const int x = lds_ld(rings + (r + 1) * kRing + ring_slot(c)) ^ ring_tag(c);
+                    const uint64_t rdy = ballot(x >= 0 && c <= drN[r]);
+                    const int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
+                    if (!(upto - dr[r] >= 16 || (upto >= drN[r] && upto > dr[r]))) break;
+                    if (c <= upto) store_granule(drOut[r] + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
+                    const bool full = upto - dr[r] == kWave;
+                    dr[r] = upto;
+                    if (lane == 0) lds_st((lds_int *)&drain[r + 1], upto);
+                    moved = true;
+                    if (!full) break;
+                }
+                drPending = drPending || dr[r] < drN[r];
+            });
+        }
         // 1. issue the granule poll (not waited for yet: the drain below runs under its latency, so
         //    the outgoing bottom row does not wait a global round trip per iteration)
         int want = 0;
@@ -1297,6 +1369,192 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, lds_int *r
     }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// DUAL fill, direction waves (R = 1, int8 text profiles, global, strip chains)
+// ------------------------------------------------------------------------------------------------
+// The strips' score waves run the recurrence alone (rec_steps_asm: 4 VALU per step instead of 7 plus
+// the bit merge), which shortens the chain's critical path; their direction planes are recomputed
+// by direction waves on the workgroups that hold no strip group. A direction task is a segment of
+// seg_len steps of one strip: its state at the segment's first step (F of the step before and the
+// diag register, the score wave's snapshot) and the strip above's bottom row (granules, written by
+// its score wave as it publishes) determine every cell of the segment, so the one-wave kernel's
+// steady bodies (sa_fill_steps.inc, no feed read, no publish) reproduce the score wave's values bit
+// for bit and write the same planes. Snapshots and granules carry the call's epoch: a task polls
+// until its data is there (no flags, no fences), and gives up like every other wait.
+__device__ __forceinline__ bool dir_poll_ok(const FillArgs &a, uint64_t &t0, uint32_t spin, int lane)
+{
+    // (data a few hundred clocks away is re-read at once; a task waiting for its strip to arrive polls
+    // about once a microsecond, so idle direction waves load the memory system little)
+    if (spin > 32) __builtin_amdgcn_s_sleep(32);
+    else if (spin > 8) __builtin_amdgcn_s_sleep(2);
+    if ((spin & 255) == 0)
+    {
+        if (t0 == 0) t0 = now_ticks();
+        else if (!keep_waiting(a, t0, lane)) return false;
+    }
+    return true;
+}
+
+template <bool HP>
+__device__ void process_dir(const FillArgs &a, int idx, int j, int lane)
+{
+    constexpr int U = 16;
+    StripDesc sd = a.strips[idx];
+    sd.pair = uniform(sd.pair);
+    sd.row0 = uniform(sd.row0);
+    sd.nsteps = uniform(sd.nsteps);
+    sd.mask_off = uniform64(sd.mask_off);
+    sd.bnd_in = uniform64(sd.bnd_in);
+    PairDesc pd = a.pairs[sd.pair];
+    pd.text_len = uniform64(pd.text_len);
+    pd.pattern_len = uniform64(pd.pattern_len);
+    pd.pattern_off = uniform64(pd.pattern_off);
+    pd.code_off = uniform64(pd.code_off);
+    pd.code_len = uniform64(pd.code_len);
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
+    const int sBeg = j * a.seg_len, sEnd = min(sBeg + a.seg_len, sd.nsteps);
+    const uint32_t epoch = a.epoch;
+    // the lane's text profile (process_strip, kArr8) and plane chunk offset
+    const int row = sd.row0 + lane;
+    int c = row <= m ? (int)a.pattern[pd.pattern_off + row - 1] : 0;
+    c = min(max(c, 0), a.A - 1);
+    const uint32_t coff = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+    const __amdgpu_buffer_rsrc_t crsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(a.masks + sd.mask_off * 4, 0, 0x7ffffff0, kBufRsrcWord3);
+    const uint32_t moff = (uint32_t)(lane * Cfg<1>::LW * 4);
+    typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+    auto load_codes = [&](int s, int (&T)[4]) __attribute__((always_inline)) {
+        const i32x4u v = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff, s, 0);
+        T[0] = v.x;
+        T[1] = v.y;
+        T[2] = v.z;
+        T[3] = v.w;
+    };
+    // feed of the body at s: lanes 0..U-1 = the strip above's bottom row at columns s+1 .. s+U
+    // (granule s + lane); lanes past column n are never needed
+    const uint64_t *fin = a.bnd + sd.bnd_in;
+    const bool feedLane = HP && lane < U;
+    auto feed_load = [&](int s) __attribute__((always_inline)) -> uint64_t {
+        return feedLane && s + lane < n ? load_granule(fin + s + lane) : ((uint64_t)epoch << 32);
+    };
+    uint64_t t0 = 0;
+    bool ok = true;
+    auto feed_take = [&](int s, uint64_t v) __attribute__((always_inline)) -> int {
+        for (uint32_t spin = 1; ok && ballot((uint32_t)(v >> 32) != epoch) != 0; ++spin)
+        {
+            ok = dir_poll_ok(a, t0, spin, lane);
+            v = feed_load(s);
+        }
+        return (int)(uint32_t)v;
+    };
+    // state at sBeg: the column-0 boundary, or the score wave's snapshot
+    int F = 0, diag = 0;
+    if (sBeg > 0)
+    {
+        const uint64_t *e = a.snap + ((size_t)idx * a.seg_stride + j) * (2 * kWave) + lane;
+        for (uint32_t spin = 1; ok; ++spin)
+        {
+            const uint64_t f = load_granule(e), d = load_granule(e + kWave);
+            if (ballot((uint32_t)(f >> 32) != epoch || (uint32_t)(d >> 32) != epoch) == 0)
+            {
+                F = (int)(uint32_t)f;
+                diag = (int)(uint32_t)d;
+                break;
+            }
+            ok = dir_poll_ok(a, t0, spin, lane);
+        }
+    }
+    int mkv[8], dX[8], dY[8];
+    sfor<8>([&](auto Gc) {
+        constexpr int g = decltype(Gc)::value;
+        dX[g] = dY[g] = 0;
+        int mk;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(mk) : "i"((int)(0x80808080u >> g)));
+        mkv[g] = mk;
+    });
+    int TA[4], TB[4], TC[4], TD[4];
+    uint64_t PA = 0, PB = 0, PC = 0, PD = 0;
+    load_codes(sBeg, TA);
+    load_codes(sBeg + U, TB);
+    if constexpr (HP)
+    {
+        PA = feed_load(sBeg);
+        PB = feed_load(sBeg + U);
+    }
+    auto body = [&](auto half, int s, int (&T)[4], uint64_t P) __attribute__((always_inline)) {
+        constexpr int HALF = decltype(half)::value;
+        StepRegs r;
+        if constexpr (HP) r.Q = feed_take(s, P);
+        else asm volatile("v_mov_b32 %0, 0" : "=v"(r.Q));  // row 0 (opaque: see process_strip's feed)
+        r.diag = diag;
+        r.F = F;
+        sfor<8>([&](auto Gc) {
+            constexpr int g = decltype(Gc)::value;
+            r.X[g] = dX[g];
+            r.Y[g] = dY[g];
+        });
+        sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
+        steps_asm<false, false, false, HALF>(r);
+        diag = r.diag;
+        F = r.F;
+        sfor<8>([&](auto Gc) {
+            constexpr int g = decltype(Gc)::value;
+            dX[g] = r.X[g];
+            dY[g] = r.Y[g];
+        });
+        if constexpr (HALF == 1)
+        {
+            sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
+            merge_asm<false>(r);
+            // the chunk of steps s - U .. s + U - 1 (slots 32 * chunk ...)
+            const int chunk = (s + U) / 32 - 1;
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{r.acc0, r.acc1}, mrsrc, moff, chunk * (kWave * Cfg<1>::LW * 4), 0);
+        }
+    };
+    using H0 = std::integral_constant<int, 0>;
+    using H1 = std::integral_constant<int, 1>;
+    int s = sBeg;
+    for (; s + 2 * U < sEnd; s += 4 * U)
+    {
+        load_codes(s + 2 * U, TC);
+        if constexpr (HP) PC = feed_load(s + 2 * U);
+        body(H0{}, s, TA, PA);
+        load_codes(s + 3 * U, TD);
+        if constexpr (HP) PD = feed_load(s + 3 * U);
+        body(H1{}, s + U, TB, PB);
+        load_codes(s + 4 * U, TA);
+        if constexpr (HP) PA = feed_load(s + 4 * U);
+        body(H0{}, s + 2 * U, TC, PC);
+        load_codes(s + 5 * U, TB);
+        if constexpr (HP) PB = feed_load(s + 5 * U);
+        body(H1{}, s + 3 * U, TD, PD);
+    }
+    if (s < sEnd)
+    {
+        body(H0{}, s, TA, PA);
+        body(H1{}, s + U, TB, PB);
+    }
+}
+
+// Direction workers: every compute wave takes tasks from the list until it is exhausted (or the
+// launch has given up)
+__device__ __forceinline__ void dir_worker(const FillArgs &a, int lane)
+{
+    while (true)
+    {
+        int t = 0;
+        if (lane == 0) t = (int)atomicAdd(&a.ctrl->dir_head, 1u);
+        t = uniform(t);
+        if (t >= a.num_dir_tasks) break;
+        if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+        const int idx = uniform(a.dir_tasks[2 * t]), j = uniform(a.dir_tasks[2 * t + 1]);
+        if (uniform(a.strips[idx].flags) & kHasPrev) process_dir<true>(a, idx, j, lane);
+        else process_dir<false>(a, idx, j, lane);
+    }
+}
+
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
@@ -1313,6 +1571,16 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
     const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0);
     if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
+    // DUAL fill: the workgroups past the score workgroups are direction workers (no LDS, no barriers)
+    constexpr bool kDual = R == 1 && SK == kArr8 && !LOCAL && CHAIN;
+    if constexpr (kDual)
+        if (a.dual && (int)blockIdx.x >= a.score_wgs)
+        {
+#if !(defined(SA_EXPERIMENT) && defined(SA_EXP_NO_DIRWORK))
+            if (w < W) dir_worker(a, lane);  // (timing ablation: no direction work at all)
+#endif
+            return;
+        }
     while (true)
     {
         __syncthreads();  // every wave is done with the previous group's rings
@@ -1322,7 +1590,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
             H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
             H.nwaves = W;
         }
-        if (threadIdx.x <= kMaxWaves) H.cons[threadIdx.x] = 0;
+        if (threadIdx.x <= kMaxWaves) H.cons[threadIdx.x] = H.drain[threadIdx.x] = 0;
         if constexpr (CHAIN)
         {
             // tags: a zeroed ring matches no column (ring_tag)
@@ -1335,7 +1603,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         if (grp >= a.num_groups) break;
         if (CHAIN && w == W)
         {
-            io_wave(a, H.cons, rings, grp, W, lane);
+            io_wave(a, H.cons, H.drain, rings, grp, W, lane);
         }
         else
         {
@@ -1346,8 +1614,25 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
                 // variant is instantiated, which keeps the register count of the batch kernel down)
                 const int f = uniform(a.strips[idx].flags) & (kHasPrev | kHasNext);
-                const StripLds L{H.S, H.cons, H.nwaves, nullptr, nullptr, nullptr};
-                if constexpr (CHAIN)
+                const StripLds L{H.S, H.cons, H.nwaves, nullptr, nullptr, nullptr, H.drain};
+                if constexpr (kDual)
+                {
+                    if (a.dual)
+                    {
+                        if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true, false, true>(a, L, rings, idx, w, lane);
+                        else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false, false, true>(a, L, rings, idx, w, lane);
+                        else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true, false, true>(a, L, rings, idx, w, lane);
+                        else process_strip<R, LOCAL, SK, false, false, false, true>(a, L, rings, idx, w, lane);
+                    }
+                    else
+                    {
+                        if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
+                        else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
+                        else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, L, rings, idx, w, lane);
+                        else process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
+                    }
+                }
+                else if constexpr (CHAIN)
                 {
                     if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
                     else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);

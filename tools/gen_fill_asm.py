@@ -46,14 +46,15 @@ steps: keys alternate between two registers); the caller adds the body's key bas
 import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, "sequence-alignment-gpu_amd", "csrc", "sa_fill_steps.inc")
+OUT = os.environ.get("SA_GEN_FILL_OUT") or os.path.join(ROOT, "sequence-alignment-gpu_amd", "csrc", "sa_fill_steps.inc")
+
 
 U = 16
 # with a strip above, the next body's feed read is issued after this step (kPfLead = U - PF_STEP)
 PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "14"))
 
 
-def block(local: bool, hn: bool, hp: bool, half: int) -> str:
+def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) -> str:
     # named operands (the C++ wrapper below binds them)
     A, B, C, FA = "%[q]", "%[qn]", "%[dg]", "%[f]"
     D, M, T0 = "%[d]", "%[m]", "%[t0]"
@@ -83,6 +84,13 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf")
         else:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        if rec_only:
+            # b, d, c, max3: c (DPP of F) stands two instructions behind the max3 that wrote F
+            out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
+                       f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
+            out.append(f"v_mov_b32_dpp {qr}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
+            out.append(f"v_max3_i32 {dg}, {D}, {fp}, {qr}")
+            continue
         out.append(f"v_mov_b32_dpp {qr}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
         out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
                    f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
@@ -154,10 +162,11 @@ def merge(local: bool) -> str:
     return "\\n\\t".join(out)
 
 
-def operands(local: bool, hn: bool, hp: bool):
+def operands(local: bool, hn: bool, hp: bool, rec_only: bool = False):
     outs = ['[q] "+v"(r.Q)', '[qn] "=&v"(r.Qn)', '[dg] "+v"(r.diag)', '[f] "+v"(r.F)',
             '[d] "=&v"(D)', '[m] "=&v"(M)', '[t0] "=&v"(t0)']
-    outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
+    if not rec_only:
+        outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
     ins = [f'[tw{i}] "v"(r.T[{i}])' for i in range(4)]
     if local:
         outs += [f'[z{g}] "+v"(r.Z[{g}])' for g in range(8)]
@@ -183,9 +192,26 @@ def main():
         "// of its chunk); Q / Qn / diag / F rotate through the roles with period 4 (back in place after",
         "// the body); with HP the next body's feed read (address r.pfaddr) is issued after step 12 and",
         "// waited for at the end (result r.pf). merge_asm<LOCAL>(r) builds the chunk's two words.",
+        "// rec_steps_asm<HN, HP>(r): the dual fill's score-wave steps (global, no direction bits).",
         "#pragma once",
         "",
     ]
+    # the dual fill's score waves (global): the recurrence alone, F = max3(D, left, up), 4 VALU per
+    # step (b, d, c, max3: the up-DPP c stands two instructions behind the max3 that wrote F)
+    for hn in (False, True):
+        for hp in (False, True):
+            body = block(False, hn, hp, 0, rec_only=True)
+            outs, ins = operands(False, hn, hp, rec_only=True)
+            lines.append(f"template <> __device__ __forceinline__ void rec_steps_asm<{str(hn).lower()}, "
+                         f"{str(hp).lower()}>(StepRegs &r)")
+            lines.append("{")
+            lines.append("    int D, M, t0;")
+            lines.append(f"    asm volatile(\"{body}\"")
+            lines.append("        : " + ", ".join(outs))
+            lines.append("        : " + ", ".join(ins) + (" : \"scc\");" if hp else ");"))
+            lines.append("    (void)D; (void)M; (void)t0;")
+            lines.append("}")
+            lines.append("")
     for local in (False, True):
         for hn in (False, True):
             for hp in (False, True):
