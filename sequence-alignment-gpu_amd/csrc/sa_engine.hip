@@ -193,7 +193,8 @@ struct Knobs {
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
     bool split = false;             // SA_SPLIT=1: score + dir wave per strip for R = 1 global chains
     int split_w = 2;                // SA_SPLIT_W: strips per split workgroup (1..3)
-    bool dual = false;              // SA_DUAL=1: score waves + direction tasks (sa_fill.hip, DUAL)
+    int dual = -1;                  // SA_DUAL: 1 / 0 force the dual fill (score waves + direction
+                                    // tasks, sa_fill.hip) on / off; default: texts of >= 8192 columns
     int dual_seg = 1024;            // SA_DUAL_SEG: steps per direction task (a multiple of 64)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
@@ -214,7 +215,7 @@ const Knobs &knobs()
         v.no_pair16 = get("SA_NO_PAIR16") != nullptr;
         v.split = get("SA_SPLIT") != nullptr && std::atoi(get("SA_SPLIT")) != 0;
         if (const char *e = get("SA_SPLIT_W")) v.split_w = std::min(3, std::max(1, std::atoi(e)));
-        if (const char *e = get("SA_DUAL")) v.dual = std::atoi(e) != 0;
+        if (const char *e = get("SA_DUAL")) v.dual = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_DUAL_SEG"))
         {
             // a power of two, at least 64 (the score waves test segment starts with a mask)
@@ -758,9 +759,14 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         pl->W = knobs().split_w;
     }
     // the dual fill: the same chains, when the strip groups leave at least half of the CUs to the
-    // direction waves (one workgroup per CU, so no CU runs both)
+    // direction waves (one workgroup per CU, so no CU runs both); by default for texts of at least
+    // 8192 columns (4096-column protein measured 4 % slower dual: its chain is too short to win back
+    // the segment tail)
     const int64_t groups = ((int64_t)pl->strips.size() + pl->W - 1) / pl->W;
-    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && !pl->split && knobs().dual &&
+    uint64_t nlong = 0;
+    for (const PairDesc &d : pl->pairs) nlong = std::max<uint64_t>(nlong, d.text_len);
+    const bool dualWanted = knobs().dual == 1 || (knobs().dual < 0 && nlong >= 8192);
+    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && !pl->split && dualWanted &&
         groups <= pl->num_cu / 2)
     {
         pl->dual = true;

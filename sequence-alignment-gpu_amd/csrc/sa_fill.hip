@@ -88,7 +88,7 @@ constexpr int kRingMask = kRing - 1;
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK) || defined(SA_EXP_DUAL_CSTORE)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -157,6 +157,7 @@ __device__ __forceinline__ int ring_tag(int c) { return (int)((((uint32_t)(c + 6
 __device__ __forceinline__ int ring_tag_raw(int c) { return (int)((uint32_t)(c + 63) << 20); }
 static_assert(kRing == 2048, "ring_tag assumes 2048-entry rings");
 constexpr int kConsEvery = 256;  // a consumer publishes its consumption word every this many columns
+constexpr int kIoWin = 4;        // I/O wave: 64-column windows polled / drained per round
 
 
 // a + sign_extend(byte B of w), one VALU op
@@ -644,7 +645,9 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 #endif
                     consKnown = uniform(lds_ld(consOut));
                     // dual: the I/O wave copies this ring to granules too and must have read a slot
+#if !(defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE))
                     if constexpr (DUALS) consKnown = min(consKnown, uniform(lds_ld((lds_int *)&L.drain[w + 1])));
+#endif
                     if (cLast - kRing <= consKnown) break;
                     __builtin_amdgcn_s_sleep(1);
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
@@ -655,6 +658,21 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     // DUAL score wave: every seg_len steps its state (F of the step before, diag) goes to the strip's
     // snapshot entry (its bottom row reaches the granules through the I/O wave, io_wave)
     const uint32_t epochv = a.epoch;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
+    // experiment: the compute wave stores its published bottom rows to its granules itself
+    const __amdgpu_buffer_rsrc_t brsrc =
+        __builtin_amdgcn_make_buffer_rsrc(a.bnd + (DUALS && HN ? sd.bnd_out : 0), 0, (int)(8 * pd.text_len), kBufRsrcWord3);
+    const uint32_t browOff = lane >= kWave - U ? (uint32_t)(lane - (kWave - U)) * 8u : 0x80000000u;
+#endif
+    auto brow_store = [&](int s0, int qv) __attribute__((always_inline)) {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
+        if constexpr (DUALS && HN)
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)qv, epochv}, brsrc, browOff + (uint32_t)(s0 - 64) * 8u, 0, kAuxSc1);
+#else
+        (void)s0;
+        (void)qv;
+#endif
+    };
     auto snapshot = [&](int s0, int f, int dg) __attribute__((always_inline)) {
         if constexpr (DUALS)
             if (s0 > 0 && (s0 & (a.seg_len - 1)) == 0)  // (seg_len: a power of two)
@@ -840,6 +858,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             Q = r.Q;
             upPrev = r.diag;
             F[0] = r.F;
+            if constexpr (DUALS) brow_store(s0, r.Qn);
             if constexpr (!DUALS)
                 sfor<8>([&](auto Gc) {
                     constexpr int g = decltype(Gc)::value;
@@ -1253,96 +1272,68 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain
     // slots of columns -63..0 are never copied in: give them their lap-0 tag, or the zeroed entries
     // would pass for lap-1 columns 1985..2048 (a compute-wave producer publishes from column -63)
     if (nIn > 0) lds_st(r0 + ring_slot(lane - 63), ring_tag(lane - 63));
-    // dual: rings 1 .. wl-1 (fed by strips first .. last-1) go to those strips' granules as well, the
-    // direction waves' feed (the compute waves publish into LDS only)
-    int dr[kMaxWaves - 1], drN[kMaxWaves - 1];
-    uint64_t *drOut[kMaxWaves - 1];
-    bool drPending = false;
-    sfor<kMaxWaves - 1>([&](auto Rc) {
-        constexpr int r = decltype(Rc)::value;  // ring r + 1, strip first + r
-        dr[r] = 0;
-        drN[r] = 0;
-        drOut[r] = a.bnd;
-        if (a.dual && r + 1 < wl)
-        {
-            const StripDesc sr = a.strips[first + r];
-            if (uniform(sr.flags) & kHasNext)
-            {
-                drN[r] = (int)uniform64(a.pairs[uniform(sr.pair)].text_len);
-                drOut[r] = a.bnd + uniform64(sr.bnd_out);
-                drPending = true;
-            }
-        }
-    });
-    if (nIn == 0 && nOut == 0 && !drPending) return;
+    if (nIn == 0 && nOut == 0) return;
     uint64_t t0 = now_ticks();
-    for (uint32_t spin = 1; copied < nIn || drained < nOut || drPending; ++spin)
+    for (uint32_t spin = 1; copied < nIn || drained < nOut; ++spin)
     {
         bool moved = false;
-        if (drPending)
-        {
-            drPending = false;
-            sfor<kMaxWaves - 1>([&](auto Rc) {
-                constexpr int r = decltype(Rc)::value;
-                // (up to 4 x 64 columns per pass: the score waves outrun one window per poll round trip)
-                for (int rep = 0; rep < 4 && dr[r] < drN[r]; ++rep)
-                {
-                    const int c = dr[r] + lane + 1;
-                    const int x = lds_ld(rings + (r + 1) * kRing + ring_slot(c)) ^ ring_tag(c);
-                    const uint64_t rdy = ballot(x >= 0 && c <= drN[r]);
-                    const int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
-                    if (!(upto - dr[r] >= 16 || (upto >= drN[r] && upto > dr[r]))) break;
-                    if (c <= upto) store_granule(drOut[r] + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
-                    const bool full = upto - dr[r] == kWave;
-                    dr[r] = upto;
-                    if (lane == 0) lds_st((lds_int *)&drain[r + 1], upto);
-                    moved = true;
-                    if (!full) break;
-                }
-                drPending = drPending || dr[r] < drN[r];
-            });
-        }
         // 1. issue the granule poll (not waited for yet: the drain below runs under its latency, so
         //    the outgoing bottom row does not wait a global round trip per iteration)
         int want = 0;
-        uint64_t v = 0;
+        // (kIoWin windows of 64 columns per poll: a round trip with stores in flight takes longer than
+        // a fast producer needs for one window)
+        uint64_t v[kIoWin];
         if (copied < nIn)
         {
             // ring[0]'s consumer publishes its consumption every kConsEvery columns
             const int room = uniform(lds_ld(cons0)) + kRing - copied;  // free ring slots
-            want = min(min(kWave, nIn - copied), room);
-            if (want >= min(16, nIn - copied))
-                // every poll loads the whole window (one round trip from the producer's store to
-                // the ring; a lane-0 probe first would add a second): 512 bytes per poll per waiting
-                // group is nothing next to the fill's own traffic
-                v = lane < want ? load_granule(bin + copied + lane) : 0;
-            else
-                want = 0;
+            want = min(min(kIoWin * kWave, nIn - copied), room);
+            if (want < min(16, nIn - copied)) want = 0;
         }
-        // 2. drain ring[W'] into granules for the next group
-        if (drained < nOut)
+        // every poll loads whole windows (one round trip from the producer's store to the ring; a
+        // lane-0 probe first would add a second): a few KiB per poll per waiting group is nothing
+        // next to the fill's own traffic
+        sfor<kIoWin>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            v[q] = q * kWave + lane < want ? load_granule(bin + copied + q * kWave + lane) : 0;
+        });
+        // 2. drain ring[W'] into granules for the next group (up to kIoWin windows)
+        for (int rep = 0; rep < kIoWin && drained < nOut; ++rep)
         {
             const int c = drained + lane + 1;
             const int x = lds_ld(rl + ring_slot(c)) ^ ring_tag(c);
             const uint64_t rdy = ballot(x >= 0 && c <= nOut);
             const int upto = drained + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
-            if (upto - drained >= 16 || (upto >= nOut && upto > drained))
+            if (!(upto - drained >= 16 || (upto >= nOut && upto > drained))) break;
+            if (c <= upto) store_granule(bout + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
+            const bool full = upto - drained == kWave;
+            drained = upto;
+            if (lane == 0)
             {
-                if (c <= upto) store_granule(bout + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
-                drained = upto;
-                if (lane == 0) lds_st(consL, drained);
-                moved = true;
+                lds_st(consL, drained);
+                lds_st((lds_int *)&drain[wl], drained);  // (dual: the producer waits for min(cons, drain))
             }
+            moved = true;
+            if (!full) break;
         }
         // 3. the poll's result -> ring[0]
+        int total = 0;  // ready prefix over the windows
+        bool open = want > 0;
+        sfor<kIoWin>([&](auto Qc) {
+            constexpr int q = decltype(Qc)::value;
+            if (!open) return;
+            const uint64_t rdy = ballot(q * kWave + lane < want && (uint32_t)(v[q] >> 32) == a.epoch);
+            const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);
+            const int c = copied + q * kWave + lane + 1;
+            if (lane < cnt && (total + cnt >= min(16, nIn - copied))) lds_st(r0 + ring_slot(c), (int)(uint32_t)v[q] | ring_tag(c));
+            total += cnt;
+            open = cnt == kWave;
+        });
         if (want > 0)
         {
-            const uint64_t rdy = ballot(lane < want && (uint32_t)(v >> 32) == a.epoch);
-            const int cnt = ~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy);  // ready prefix
+            const int cnt = total;
             if (cnt >= min(16, nIn - copied))
             {
-                const int c = copied + lane + 1;
-                if (lane < cnt) lds_st(r0 + ring_slot(c), (int)(uint32_t)v | ring_tag(c));
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_PROGRESS)
                 // I/O progress stamps: when ring[0] got column 4096q (timeline words 16..25 of
                 // the group's first strip)
@@ -1363,7 +1354,11 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain
         {
             // release the producer so the group drains (the launch reports the abort; ring[0]'s
             // consumer gives up by itself)
-            if (lane == 0) lds_st(consL, nOut + kRing);
+            if (lane == 0)
+            {
+                lds_st(consL, nOut + kRing);
+                lds_st((lds_int *)&drain[wl], nOut + kRing);
+            }
             return;
         }
     }
@@ -1555,11 +1550,88 @@ __device__ __forceinline__ void dir_worker(const FillArgs &a, int lane)
     }
 }
 
+
+// DUAL fill: the drain wave of a score workgroup copies the in-group rings 1 .. wl-1 (fed by strips
+// first .. last-1) to those strips' granules, the direction waves' feed; the I/O wave still drains the
+// last ring. A wave of its own: its write-through stores would otherwise sit in the I/O wave's vmcnt
+// in front of every granule poll (in-order completion) and slow the cross-group hand-off.
+__device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_int *rings, int grp, int W, int lane)
+{
+    const int first = grp * W;
+    const int last = min(first + W, a.num_strips) - 1;
+    const int wl = last - first + 1;
+    // dual: rings 1 .. wl-1 (fed by strips first .. last-1) go to those strips' granules as well, the
+    // direction waves' feed (the compute waves publish into LDS only)
+    int dr[kMaxWaves - 1], drN[kMaxWaves - 1];
+    uint64_t *drOut[kMaxWaves - 1];
+    bool drPending = false;
+    sfor<kMaxWaves - 1>([&](auto Rc) {
+        constexpr int r = decltype(Rc)::value;  // ring r + 1, strip first + r
+        dr[r] = 0;
+        drN[r] = 0;
+        drOut[r] = a.bnd;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
+        if (false)
+#else
+        if (r + 1 < wl)
+#endif
+        {
+            const StripDesc sr = a.strips[first + r];
+            if (uniform(sr.flags) & kHasNext)
+            {
+                drN[r] = (int)uniform64(a.pairs[uniform(sr.pair)].text_len);
+                drOut[r] = a.bnd + uniform64(sr.bnd_out);
+                drPending = true;
+            }
+        }
+    });
+    uint64_t t0 = now_ticks();
+    for (uint32_t spin = 1; drPending; ++spin)
+    {
+        bool moved = false;
+        if (drPending)
+        {
+            drPending = false;
+            sfor<kMaxWaves - 1>([&](auto Rc) {
+                constexpr int r = decltype(Rc)::value;
+                // (up to 4 x 64 columns per pass: the score waves outrun one window per poll round trip)
+                for (int rep = 0; rep < 4 && dr[r] < drN[r]; ++rep)
+                {
+                    const int c = dr[r] + lane + 1;
+                    const int x = lds_ld(rings + (r + 1) * kRing + ring_slot(c)) ^ ring_tag(c);
+                    const uint64_t rdy = ballot(x >= 0 && c <= drN[r]);
+                    const int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
+                    if (!(upto - dr[r] >= 16 || (upto >= drN[r] && upto > dr[r]))) break;
+                    if (c <= upto) store_granule(drOut[r] + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
+                    const bool full = upto - dr[r] == kWave;
+                    dr[r] = upto;
+                    if (lane == 0) lds_st((lds_int *)&drain[r + 1], upto);
+                    moved = true;
+                    if (!full) break;
+                }
+                drPending = drPending || dr[r] < drN[r];
+            });
+        }
+        if (moved)
+        {
+            t0 = now_ticks();
+            continue;
+        }
+        for (int z = 0; z < a.io_sleep; ++z) __builtin_amdgcn_s_sleep(1);
+        if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
+        {
+            if (lane == 0)
+                for (int r = 1; r < wl; ++r) lds_st((lds_int *)&drain[r], 1 << 30);  // release the producers
+            return;
+        }
+    }
+}
+
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
 template <int R, bool LOCAL, int SK, bool CHAIN>
-__global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs a)
+__global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
     GroupHdr &H = *reinterpret_cast<GroupHdr *>(lds_dyn);
@@ -1568,7 +1640,8 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
     const int w = uniform((int)(threadIdx.x / kWave));
     // compute waves; with CHAIN wave W is the I/O wave (plans without strip chains have none, and no
     // rings in LDS either: more workgroups fit a CU)
-    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0);
+    // (dual: one more wave, the drain wave W + 1)
+    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0) - (CHAIN && a.dual ? 1 : 0);
     if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
     // DUAL fill: the workgroups past the score workgroups are direction workers (no LDS, no barriers)
@@ -1604,6 +1677,10 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1)) void fill_kernel(FillArgs 
         if (CHAIN && w == W)
         {
             io_wave(a, H.cons, H.drain, rings, grp, W, lane);
+        }
+        else if (CHAIN && w == W + 1)
+        {
+            drain_wave(a, H.drain, rings, grp, W, lane);
         }
         else
         {
@@ -1668,7 +1745,7 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1)), lds, st, a);
+        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1 + (a.dual ? 1 : 0))), lds, st, a);
     }
     else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
 }
