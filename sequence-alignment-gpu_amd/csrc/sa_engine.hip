@@ -195,7 +195,8 @@ struct Knobs {
     int split_w = 2;                // SA_SPLIT_W: strips per split workgroup (1..3)
     int dual = -1;                  // SA_DUAL: 1 / 0 force the dual fill (score waves + direction
                                     // tasks, sa_fill.hip) on / off; default: texts of >= 8192 columns
-    int dual_seg = 1024;            // SA_DUAL_SEG: steps per direction task (a multiple of 64)
+    int dual_seg = 0;               // SA_DUAL_SEG: steps per direction task (a power of two >= 64;
+                                    // default 2048, 1024 for texts under 16384 columns)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
@@ -770,7 +771,9 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         groups <= pl->num_cu / 2)
     {
         pl->dual = true;
-        pl->seg_len = knobs().dual_seg;
+        // (measured: 2048-step segments 1.566 ms at 32768^2 against 1.60 with 1024, fewer
+        // snapshots; 8192^2 prefers 1024, its last segment's tail is a larger share)
+        pl->seg_len = knobs().dual_seg ? knobs().dual_seg : nlong >= 16384 ? 2048 : 1024;
         int jmax = 1;
         for (const StripDesc &sd : pl->strips) jmax = std::max(jmax, (sd.nsteps + pl->seg_len - 1) / pl->seg_len);
         pl->seg_stride = jmax;
