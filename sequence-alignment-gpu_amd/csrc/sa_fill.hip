@@ -1685,6 +1685,9 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
         else
         {
             const int idx = grp * W + w;
+            // dual: the score waves issue ahead of the I/O and drain waves sharing their SIMDs
+            // (measured -0.8 % fill, profiles/r03/dual_dev/prio_timeline.log)
+            if (CHAIN && a.dual) __builtin_amdgcn_s_setprio(2);
             if (idx < a.num_strips)
             {
                 // the strip kind is compile-time inside process_strip (branch-free body boundaries)
