@@ -52,6 +52,9 @@ OUT = os.environ.get("SA_GEN_FILL_OUT") or os.path.join(ROOT, "sequence-alignmen
 U = 16
 # with a strip above, the next body's feed read is issued after this step (kPfLead = U - PF_STEP)
 PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "14"))
+# the dual fill's score steps (rec_steps_asm) are shorter, so their read takes more steps of lead:
+# after step 10 measured 1 % faster than after 14 (profiles/r03/dual_dev/pf_timeline.log)
+REC_PF_STEP = int(os.environ.get("SA_GEN_REC_PF_STEP", "10"))
 
 
 def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) -> str:
@@ -78,7 +81,7 @@ def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) ->
         g, byte = 4 * half + (q & 3), 3 - (q >> 2)
         sd = f"dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
-        if hp and q == PF_STEP:
+        if hp and q == (REC_PF_STEP if rec_only else PF_STEP):
             out.append(f"ds_read_b32 {PF}, {PFA}")
         if hn:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf")
