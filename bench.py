@@ -13,7 +13,10 @@ traceback is timed separately and reported as e2e). With --gpus N every rank ali
 pair i -> rank i mod N, one fill + traceback per step per rank, scores gathered to rank 0 over
 RCCL (torch.distributed 'nccl'); strong scaling.
 
-Prints ONE JSON line on rank 0. Launch N>1 with torch.distributed.run (see README/DESIGN).
+Prints ONE JSON line on rank 0. `--gpus N` (N > 1) launched without WORLD_SIZE starts its N ranks
+itself (torch.distributed.run, one process per GPU, before this process touches a GPU); launched by
+torch.distributed.run, WORLD_SIZE must equal N. `--dry-run` exercises the rank plumbing only (gloo,
+no GPU work, value null): the CPU test of the launcher.
 """
 from __future__ import annotations
 
@@ -58,6 +61,8 @@ def parse():
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
     ap.add_argument("--batch-chunks", type=int, default=1,
                     help="batch: plans per rank; chunk k's traceback overlaps chunk k+1's fill")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rank plumbing only (gloo, no GPU): launch / barrier / max-over-ranks / rank-0 line")
     ap.add_argument("--native", action="store_true",
                     help="batch: one process drives the C++ sa_align_batch over --gpus devices (host inputs, "
                          "per-device threads and plans, results gathered over RCCL); no torch.distributed")
@@ -180,6 +185,13 @@ class Chunked:
         if two:
             self.s_fill.wait_stream(self.s_tb)
 
+    def copy_results(self, buf) -> None:
+        """Every plan's sa_result array, device to device, into the rows of buf (a (k, 4) int64 tensor)."""
+        row = 0
+        for j in self.jobs:
+            j.plan.copy_results(buf.data_ptr() + 32 * row, self.s_fill.cuda_stream)
+            row += j.plan.num_pairs
+
     def results(self) -> np.ndarray:
         """Every pair's sa_result (numpy structured array; one copy per plan, no per-pair objects)."""
         return np.concatenate([j.plan.results_array(self.s_fill.cuda_stream) for j in self.jobs])
@@ -217,8 +229,65 @@ def main_native(args) -> None:
     }), flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> None:
+    """One rank process per GPU through torch.distributed.run (127.0.0.1 rendezvous), started from
+    this process before it has made any GPU call; exits with the launcher's status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    raise SystemExit(subprocess.call(cmd, env=env))
+
+
+def main_dry_run(args) -> None:
+    """--dry-run: the multi-rank plumbing of main() without the engine (gloo on the CPU)."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    for _ in range(args.warmup):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        time.sleep(0.001)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRICS[args.workload], "value": None, "unit": "GCUPS", "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+                          "dry_run": True, "ranks_seen": world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and args.gpus > 1 and not args.native:
+        launch_ranks(args.gpus)
+    if ws is not None and int(ws) != args.gpus and not args.native:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}: launch one rank per GPU "
+                         f"(torch.distributed.run --nproc-per-node {args.gpus}) or drop WORLD_SIZE")
+    if args.dry_run:
+        main_dry_run(args)
+        return
     if args.native:
         if args.workload != "batch" or int(os.environ.get("WORLD_SIZE", "1")) > 1:
             raise SystemExit("--native: --workload batch in one process (it drives --gpus devices itself)")
@@ -279,6 +348,8 @@ def main():
         chunks = [DeviceBatch(0, S, gap, texts[a:b], pats[a:b], device=local, rows_per_lane=args.rows_per_lane)
                   for a, b in zip(cuts, cuts[1:]) if b > a]
         job = Chunked(chunks, torch, local)
+        # the rank's sa_result rows go device to device into this buffer and on to rank 0 (RCCL gather)
+        gbuf = torch.full(((npairs + world - 1) // world, 4), -1, dtype=torch.int64, device=torch.device("cuda", local))
         cells_rank = len(mine) * L * L
         pairs_rank = len(mine)
         workload = {"workload": f"dna_global_batch_{npairs}x{L}x{L}", "pairs_total": npairs, "text_len": L,
@@ -300,9 +371,13 @@ def main():
             # a second stream, overlapping chunk k+1's fill), results to host, and the path's exchange
             # step — every rank's results gathered to rank 0 over RCCL (xGMI)
             job.fill_and_traceback(ev)
-            r = job.results()
             if world > 1:
-                distributed.gather_array(r, npairs, world, rank, dev)
+                # results device to device into the gather buffer, gathered to rank 0 over RCCL and
+                # brought to rank 0's host there (no D2H -> H2D hop before the collective)
+                job.copy_results(gbuf)
+                distributed.gather_device(gbuf, npairs, world, rank)
+            else:
+                job.results()
         else:
             job.fill(ev)
 
@@ -348,7 +423,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tmax = float(tt.item())
         if args.workload == "batch":
-            allres = distributed.gather_array(res, npairs, world, rank, dev)
+            job.copy_results(gbuf)
+            allres = distributed.gather_device(gbuf, npairs, world, rank)
             if rank == 0:
                 scores = allres[:, 0].tolist()
     cells_total = cells_rank * world

@@ -102,7 +102,10 @@ typedef struct sa_host_pair {
  * with RCCL, loaded on first use, communicators kept for the process). Synchronous. results: num_pairs entries. aligned_text / aligned_pattern: NULL (scores only) or
  * num_pairs host buffers, buffer i of at least text_len + pattern_len bytes, receiving pair i's
  * num_alignment_bytes letters in forward order. The pair -> device deal is sa_batch_deal's. If
- * num_gpus exceeds the device count, devices are shared round-robin (no RCCL then). */
+ * num_gpus exceeds the device count, devices are shared round-robin (no RCCL then).
+ * Calls are serialised process-wide (one batch at a time, whatever the devices). Each shard keeps its
+ * stream, device arenas, RCCL buffers and plan across calls; a call whose shards have the same pair
+ * shapes and scoring parameters as the previous one reuses the plans. */
 int sa_align_batch(const sa_params *params, const sa_host_pair *pairs, int64_t num_pairs, int num_gpus,
                    sa_result *results, char *const *aligned_text, char *const *aligned_pattern);
 
@@ -164,6 +167,11 @@ int sa_plan_fetch_directions(sa_plan *plan, int64_t index, uint8_t *M_out, void 
 
 /* Device pointer to the per-pair sa_result array written by sa_plan_traceback. */
 const void *sa_plan_device_results(const sa_plan *plan);
+
+/* Copies the per-pair sa_result array (num_pairs * sizeof(sa_result) bytes) to device memory d_dst
+ * on `stream` (asynchronous, device to device: the batch path's results go to the RCCL gather without
+ * a host round trip). The abort / bad-input flags are not checked here (sa_plan_fetch_results does). */
+int sa_plan_copy_results(const sa_plan *plan, void *d_dst, void *stream);
 
 /* ---- misc ------------------------------------------------------------------------------ */
 int sa_device_count(int *count);

@@ -14,9 +14,13 @@
 //     (ncclGather over xGMI) and the caller's results come from that gathered buffer only; the
 //     strings are copied into the caller's buffers after it, with the gathered lengths. RCCL is
 //     loaded on first use (dlopen: callers that never shard over several devices do not need it)
-//     and the communicators of a device set are created once per process. Shards that share a
-//     device (num_gpus > device count, a test mode for one-GPU machines) skip RCCL and take their
-//     results from their own plan.
+//     and the communicators of a device set are created once per process (and dropped after a failed
+//     gather, so the next call rebuilds them). Shards that share a device (num_gpus > device count, a
+//     test mode for one-GPU machines) skip RCCL and take their results from their own plan;
+//   * per shard slot, a cache that lives across calls: its stream, its device input arenas and RCCL
+//     send buffer (grow-only), and its plan, reused while the shard's pair shapes and the scoring
+//     parameters stay the same (a repeated batch costs its uploads, kernels and copies only), plus
+//     the gather buffer on device 0. Calls are serialised process-wide (g_batch_mu).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -83,6 +87,88 @@ Rccl &rccl()
 // at exit; destroying them from a static destructor can run after the HIP runtime is gone).
 std::map<int, std::vector<ncclComm_t>> g_comms;
 
+// ---- per-shard caches (across calls) ------------------------------------------------------------
+struct ShardCache {
+    int device = -1;
+    hipStream_t st = nullptr;
+    char *dt = nullptr, *dp = nullptr;  // input arenas
+    size_t dt_cap = 0, dp_cap = 0;
+    sa_result *d_send = nullptr;        // RCCL send buffer
+    size_t send_cap = 0;
+    sa_plan *plan = nullptr;            // the last plan and what it was built for
+    std::vector<sa_pair> plan_pairs;
+    std::vector<int32_t> plan_params;   // mode, A, gap, rows_per_lane, the matrix, the alphabet bytes
+};
+std::vector<ShardCache> g_cache;
+sa_result *g_gather = nullptr;  // device 0
+size_t g_gather_cap = 0;
+
+void free_cache_slot(ShardCache &c)
+{
+    if (c.device < 0) return;
+    (void)hipSetDevice(c.device);
+    if (c.plan) sa_plan_destroy(c.plan);
+    if (c.dt) (void)hipFree(c.dt);
+    if (c.dp) (void)hipFree(c.dp);
+    if (c.d_send) (void)hipFree(c.d_send);
+    if (c.st) (void)hipStreamDestroy(c.st);
+    c = ShardCache();
+}
+
+void release_batch_cache()
+{
+    std::lock_guard<std::mutex> lock(g_batch_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (ShardCache &c : g_cache) free_cache_slot(c);
+    g_cache.clear();
+    if (g_gather)
+    {
+        (void)hipSetDevice(0);
+        (void)hipFree(g_gather);
+    }
+    g_gather = nullptr;
+    g_gather_cap = 0;
+    (void)hipSetDevice(cur);
+}
+
+// grow-only device buffer (contents not kept)
+template <typename T>
+bool ensure(T **p, size_t &cap, size_t bytes)
+{
+    if (cap >= bytes && *p) return true;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    if (hipMalloc((void **)p, bytes) != hipSuccess)
+    {
+        (void)hipGetLastError();
+        *p = nullptr;
+        return false;
+    }
+    cap = bytes;
+    return true;
+}
+
+std::vector<int32_t> params_key(const sa_params *P)
+{
+    std::vector<int32_t> k{P->mode, P->alphabet_size, P->gap_penalty, P->rows_per_lane};
+    for (int e = 0; e < P->alphabet_size * P->alphabet_size; ++e) k.push_back(P->score_matrix[e]);
+    if (P->alphabet)
+        for (int c = 0; c <= P->alphabet_size && P->alphabet[c]; ++c) k.push_back((int32_t)(unsigned char)P->alphabet[c]);
+    return k;
+}
+
+bool same_pairs(const std::vector<sa_pair> &a, const std::vector<sa_pair> &b)
+{
+    if (a.size() != b.size()) return false;
+    for (size_t q = 0; q < a.size(); ++q)
+        if (a[q].text_offset != b[q].text_offset || a[q].text_len != b[q].text_len ||
+            a[q].pattern_offset != b[q].pattern_offset || a[q].pattern_len != b[q].pattern_len)
+            return false;
+    return true;
+}
+
 // ---- shards -------------------------------------------------------------------------------------
 struct Shard {
     std::vector<int64_t> idx;  // global pair indices, in ascending order
@@ -92,8 +178,7 @@ struct Shard {
     std::vector<sa_result> res;    // own results (no RCCL only)
     std::vector<char> ot, op;      // aligned-string arenas on the host
     std::vector<uint64_t> off;     // each pair's offset in the arenas
-    sa_result *d_send = nullptr;   // RCCL send buffer (width entries), device `device`
-    hipStream_t st = nullptr;
+    ShardCache *c = nullptr;       // this shard's cache slot (stream, arenas, send buffer, plan)
     double ms = 0;
 };
 
@@ -101,9 +186,11 @@ thread_local int32_t t_last_shards = 0, t_last_rccl = 0;
 thread_local std::vector<double> t_last_ms;
 thread_local double t_last_gather_ms = 0;
 
-// Runs one shard on its device: upload, plan, fill, traceback; results into the RCCL send buffer
-// (rccl) or to the host, aligned-string arenas to the host (when the caller wants strings).
-void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, bool strings, size_t width, bool rccl_path)
+// Runs one shard on its device: upload, plan (the cached one when the shapes match), fill, traceback;
+// results into the RCCL send buffer (rccl) or to the host, aligned-string arenas to the host (when the
+// caller wants strings).
+void run_shard(const sa_params *P, const std::vector<int32_t> &pkey, const sa_host_pair *pairs, Shard &sh,
+               bool strings, size_t width, bool rccl_path)
 {
     const Clock::time_point t0 = Clock::now();
     auto bad = [&](int code, const std::string &msg) {
@@ -128,32 +215,37 @@ void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, bool st
         if (h.text_len) std::memcpy(&ht[pp[q].text_offset], h.text, h.text_len);
         if (h.pattern_len) std::memcpy(&hpat[pp[q].pattern_offset], h.pattern, h.pattern_len);
     }
-    char *dt = nullptr, *dp = nullptr;
-    sa_plan *plan = nullptr;
-    auto cleanup = [&]() {
-        if (plan) sa_plan_destroy(plan);
-        if (dt) (void)hipFree(dt);
-        if (dp) (void)hipFree(dp);
-    };
-    if (hipMalloc((void **)&dt, ht.size()) != hipSuccess || hipMalloc((void **)&dp, hpat.size()) != hipSuccess)
-    {
-        (void)hipGetLastError();
-        cleanup();
+    ShardCache &c = *sh.c;
+    if (!ensure(&c.dt, c.dt_cap, ht.size()) || !ensure(&c.dp, c.dp_cap, hpat.size()))
         return bad(SA_ERR_NOMEM, "sa_align_batch: device allocation failed");
-    }
     int rc = SA_OK;
-    if (hipMemcpyAsync(dt, ht.data(), ht.size(), hipMemcpyHostToDevice, sh.st) != hipSuccess ||
-        hipMemcpyAsync(dp, hpat.data(), hpat.size(), hipMemcpyHostToDevice, sh.st) != hipSuccess)
+    if (hipMemcpyAsync(c.dt, ht.data(), ht.size(), hipMemcpyHostToDevice, c.st) != hipSuccess ||
+        hipMemcpyAsync(c.dp, hpat.data(), hpat.size(), hipMemcpyHostToDevice, c.st) != hipSuccess)
         rc = SA_ERR_HIP;
-    if (!rc) rc = sa_plan_create(P, pp.data(), (int64_t)k, sh.device, &plan);
-    if (!rc) rc = sa_plan_fill(plan, dt, dp, sh.st);
-    if (!rc) rc = sa_plan_traceback(plan, sh.st);
+    if (!rc && !(c.plan && c.plan_params == pkey && same_pairs(c.plan_pairs, pp)))
+    {
+        if (c.plan)
+        {
+            (void)hipStreamSynchronize(c.st);  // (the old plan's last kernels are done with it)
+            sa_plan_destroy(c.plan);
+            c.plan = nullptr;
+        }
+        rc = sa_plan_create(P, pp.data(), (int64_t)k, sh.device, &c.plan);
+        if (!rc)
+        {
+            c.plan_pairs = pp;
+            c.plan_params = pkey;
+        }
+        else c.plan = nullptr;
+    }
+    sa_plan *plan = c.plan;
+    if (!rc) rc = sa_plan_fill(plan, c.dt, c.dp, c.st);
+    if (!rc) rc = sa_plan_traceback(plan, c.st);
     if (!rc && rccl_path)
     {
         // the shard's results into the fixed-width RCCL send buffer (unused entries stay zero)
-        if (hipMemsetAsync(sh.d_send, 0, width * sizeof(sa_result), sh.st) != hipSuccess ||
-            (k && hipMemcpyAsync(sh.d_send, sa_plan_device_results(plan), k * sizeof(sa_result),
-                                 hipMemcpyDeviceToDevice, sh.st) != hipSuccess))
+        if (hipMemsetAsync(c.d_send, 0, width * sizeof(sa_result), c.st) != hipSuccess ||
+            (k && sa_plan_copy_results(plan, c.d_send, c.st) != SA_OK))
             rc = SA_ERR_HIP;
     }
     if (!rc)
@@ -165,11 +257,18 @@ void run_shard(const sa_params *P, const sa_host_pair *pairs, Shard &sh, bool st
         if (!rccl_path) sh.res.resize(std::max<size_t>(1, k));
         // (also synchronises the stream: the send buffer is complete before the gather)
         rc = sa_plan_fetch_all(plan, rccl_path ? nullptr : sh.res.data(), strings ? sh.ot.data() : nullptr,
-                               strings ? sh.op.data() : nullptr, nb, sh.off.data(), sh.st);
+                               strings ? sh.op.data() : nullptr, nb, sh.off.data(), c.st);
         if (!rccl_path) sh.res.resize(k);
     }
-    if (rc) bad(rc, sa_last_error());
-    cleanup();
+    if (rc)
+    {
+        bad(rc, sa_last_error());
+        // a failed plan is not reused (a timed-out fill may have left it mid-way)
+        (void)hipStreamSynchronize(c.st);
+        if (c.plan) sa_plan_destroy(c.plan);
+        c.plan = nullptr;
+        c.plan_pairs.clear();
+    }
     sh.ms = ms_since(t0);
 }
 
@@ -249,28 +348,28 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
     t_last_gather_ms = 0;
     // RCCL only across distinct devices (one communicator per device)
     const bool use_rccl = G > 1 && G <= ndev;
-    sa_result *d_gather = nullptr;
-    auto release = [&]() {
-        for (Shard &x : sh)
-        {
-            (void)hipSetDevice(x.device);
-            if (x.d_send) (void)hipFree(x.d_send);
-            if (x.st) (void)hipStreamDestroy(x.st);
-        }
-        if (d_gather)
-        {
-            (void)hipSetDevice(0);
-            (void)hipFree(d_gather);
-        }
-        (void)hipSetDevice(cur);
-    };
-    for (Shard &x : sh)
+    auto restore = [&]() { (void)hipSetDevice(cur); };
+    // the shards' cache slots (created on first use; a slot whose device changed is rebuilt); the
+    // process frees them at exit (registered after HIP initialised, so it runs before its teardown)
+    static bool s_atexit = false;
+    if (!s_atexit)
     {
-        (void)hipSetDevice(x.device);
-        if (hipStreamCreateWithFlags(&x.st, hipStreamNonBlocking) != hipSuccess)
+        std::atexit(release_batch_cache);
+        s_atexit = true;
+    }
+    if (g_cache.size() < (size_t)G) g_cache.resize(G);
+    for (int s = 0; s < G; ++s)
+    {
+        ShardCache &c = g_cache[s];
+        if (c.device != sh[s].device) free_cache_slot(c);
+        c.device = sh[s].device;
+        sh[s].c = &c;
+        (void)hipSetDevice(c.device);
+        if (!c.st && hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess)
         {
             (void)hipGetLastError();
-            release();
+            c.st = nullptr;
+            restore();
             return fail_b(SA_ERR_HIP, "sa_align_batch: stream creation failed");
         }
     }
@@ -280,7 +379,7 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         Rccl &R = rccl();
         if (!R.ok)
         {
-            release();
+            restore();
             return fail_b(SA_ERR_HIP, "sa_align_batch: " + R.err);
         }
         auto it = g_comms.find(G);
@@ -291,7 +390,7 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
             std::vector<ncclComm_t> c(G);
             if (R.commInitAll(c.data(), G, devs.data()) != ncclSuccess)
             {
-                release();
+                restore();
                 return fail_b(SA_ERR_HIP, "sa_align_batch: ncclCommInitAll failed");
             }
             it = g_comms.emplace(G, std::move(c)).first;
@@ -300,31 +399,30 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         for (int s = 0; s < G; ++s)
         {
             (void)hipSetDevice(s);
-            if (hipMalloc((void **)&sh[s].d_send, width * sizeof(sa_result)) != hipSuccess)
+            if (!ensure(&sh[s].c->d_send, sh[s].c->send_cap, width * sizeof(sa_result)))
             {
-                (void)hipGetLastError();
-                release();
+                restore();
                 return fail_b(SA_ERR_NOMEM, "sa_align_batch: RCCL buffer allocation failed");
             }
         }
         (void)hipSetDevice(0);
-        if (hipMalloc((void **)&d_gather, (size_t)G * width * sizeof(sa_result)) != hipSuccess)
+        if (!ensure(&g_gather, g_gather_cap, (size_t)G * width * sizeof(sa_result)))
         {
-            (void)hipGetLastError();
-            release();
+            restore();
             return fail_b(SA_ERR_NOMEM, "sa_align_batch: RCCL buffer allocation failed");
         }
     }
     const bool strings = aligned_text || aligned_pattern;
+    const std::vector<int32_t> pkey = params_key(P);
     std::vector<std::thread> th;
     for (int s = 0; s < G; ++s)
-        th.emplace_back(run_shard, P, pairs, std::ref(sh[s]), strings, width, use_rccl);
+        th.emplace_back(run_shard, P, std::cref(pkey), pairs, std::ref(sh[s]), strings, width, use_rccl);
     for (std::thread &t : th) t.join();
     for (int s = 0; s < G; ++s) t_last_ms[s] = sh[s].ms;
     for (const Shard &x : sh)
         if (x.rc)
         {
-            release();
+            restore();
             return fail_b(x.rc, "sa_align_batch: shard on device " + std::to_string(x.device) + ": " + x.err);
         }
     // per-pair results: gathered over RCCL (the exchange step) or straight from each shard
@@ -335,24 +433,27 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
         Rccl &R = rccl();
         bool ok = R.groupStart() == ncclSuccess;
         for (int s = 0; s < G && ok; ++s)
-            ok = R.gather(sh[s].d_send, s == 0 ? d_gather : nullptr, width * sizeof(sa_result), ncclUint8, 0,
-                          (*comms)[s], sh[s].st) == ncclSuccess;
+            ok = R.gather(sh[s].c->d_send, s == 0 ? g_gather : nullptr, width * sizeof(sa_result), ncclUint8, 0,
+                          (*comms)[s], sh[s].c->st) == ncclSuccess;
         ok = (R.groupEnd() == ncclSuccess) && ok;
         all.resize((size_t)G * width);
         if (ok)
         {
             (void)hipSetDevice(0);
-            ok = hipMemcpyAsync(all.data(), d_gather, all.size() * sizeof(sa_result), hipMemcpyDeviceToHost,
-                                sh[0].st) == hipSuccess;
+            ok = hipMemcpyAsync(all.data(), g_gather, all.size() * sizeof(sa_result), hipMemcpyDeviceToHost,
+                                sh[0].c->st) == hipSuccess;
             for (int s = 0; s < G && ok; ++s)
             {
                 (void)hipSetDevice(s);
-                ok = hipStreamSynchronize(sh[s].st) == hipSuccess;
+                ok = hipStreamSynchronize(sh[s].c->st) == hipSuccess;
             }
         }
         if (!ok)
         {
-            release();
+            // a communicator left in an error state is not reused: the next call builds new ones
+            // (the failed ones are abandoned, not destroyed: their state is unknown)
+            g_comms.erase(G);
+            restore();
             return fail_b(SA_ERR_HIP, "sa_align_batch: RCCL result gather failed");
         }
         t_last_gather_ms = ms_since(tg);
@@ -370,7 +471,7 @@ int sa_align_batch(const sa_params *P, const sa_host_pair *pairs, int64_t num_pa
             if (aligned_pattern && aligned_pattern[i] && L) std::memcpy(aligned_pattern[i], &x.op[x.off[q]], L);
         }
     }
-    release();
+    restore();
     return SA_OK;
 }
 

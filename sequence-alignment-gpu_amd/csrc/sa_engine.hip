@@ -191,12 +191,9 @@ struct Knobs {
     int rows_per_lane = 0;          // SA_ROWS_PER_LANE: force R (1..32)
     int waves_per_group = 0;        // SA_WAVES_PER_GROUP: force W (1..4)
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
-    bool split = false;             // SA_SPLIT=1: score + dir wave per strip for R = 1 global chains
-    int split_w = 2;                // SA_SPLIT_W: strips per split workgroup (1..3)
-    int dual = -1;                  // SA_DUAL: 1 / 0 force the dual fill (score waves + direction
-                                    // tasks, sa_fill.hip) on / off; default: texts of >= 8192 columns
-    int dual_seg = 0;               // SA_DUAL_SEG: steps per direction task (a power of two >= 64;
-                                    // default 2048, 1024 for texts under 16384 columns)
+    int band = -1;                  // SA_BAND: 1 / 0 force the band fill (128-row score strips
+                                    // feeding the 64-row strips, sa_fill.hip process_band) on / off;
+                                    // default: on wherever it applies (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
@@ -214,16 +211,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_ROWS_PER_LANE")) v.rows_per_lane = std::atoi(e);
         if (const char *e = get("SA_WAVES_PER_GROUP")) v.waves_per_group = std::atoi(e);
         v.no_pair16 = get("SA_NO_PAIR16") != nullptr;
-        v.split = get("SA_SPLIT") != nullptr && std::atoi(get("SA_SPLIT")) != 0;
-        if (const char *e = get("SA_SPLIT_W")) v.split_w = std::min(3, std::max(1, std::atoi(e)));
-        if (const char *e = get("SA_DUAL")) v.dual = std::atoi(e) != 0 ? 1 : 0;
-        if (const char *e = get("SA_DUAL_SEG"))
-        {
-            // a power of two, at least 64 (the score waves test segment starts with a mask)
-            int sg = 64;
-            while (sg * 2 <= std::atoi(e)) sg *= 2;
-            v.dual_seg = sg;
-        }
+        if (const char *e = get("SA_BAND")) v.band = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
         if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
@@ -291,12 +279,10 @@ struct sa_plan {
     int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12, key_rowbits = 21;
     int sk = 0;          // ScoreKind of the fill
     bool chain = false;  // some pair has more than one strip
-    bool split = false;  // R = 1 int8-profile global chains: score + dir wave per strip (sa_split.inc)
-    bool dual = false;   // R = 1 int8-profile global chains: score waves + direction tasks (sa_fill.hip)
-    int seg_len = 0, seg_stride = 0;
-    std::vector<int32_t> h_tasks;  // dual: {strip, segment} pairs in the order direction waves take them
-    int32_t *d_tasks = nullptr;
-    uint64_t *d_snap = nullptr;
+    // band fill (R = 1 int8-profile chains): 128-row score strips ahead of the 64-row strips
+    bool band = false;
+    std::vector<StripDesc> bands;
+    StripDesc *d_bands = nullptr;
     int num_cu = 0;
     std::vector<PairDesc> pairs;
     std::vector<StripDesc> strips;
@@ -385,7 +371,7 @@ void free_plan(sa_plan *p)
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
-                    p->d_out_pattern, p->d_results, p->d_tasks, p->d_snap};
+                    p->d_out_pattern, p->d_results, p->d_bands};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -753,52 +739,52 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         }
         if (pair) pl->sk = kPair;
     }
-    // the split fill: R = 1 chains with int8 text profiles, global mode
-    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && knobs().split)
+    // the band fill (sa_fill.hip process_band): R = 1 chains with int8 text profiles (global, or local
+    // with g >= 0, which kArr8 implies), W even (a group boundary inside a pair must fall on a band
+    // boundary: every pair's first strip even), and the band groups plus the strip groups fit one
+    // workgroup per CU
     {
-        pl->split = true;
-        pl->W = knobs().split_w;
-    }
-    // the dual fill: the same chains, when the strip groups leave at least half of the CUs to the
-    // direction waves (one workgroup per CU, so no CU runs both); by default for texts of at least
-    // 8192 columns (4096-column protein measured 4 % slower dual: its chain is too short to win back
-    // the segment tail)
-    const int64_t groups = ((int64_t)pl->strips.size() + pl->W - 1) / pl->W;
-    uint64_t nlong = 0;
-    for (const PairDesc &d : pl->pairs) nlong = std::max<uint64_t>(nlong, d.text_len);
-    const bool dualWanted = knobs().dual == 1 || (knobs().dual < 0 && nlong >= 8192);
-    if (pl->R == 1 && pl->sk == kArr8 && pl->chain && P->mode == SA_GLOBAL && !pl->split && dualWanted &&
-        groups <= pl->num_cu / 2)
-    {
-        pl->dual = true;
-        // (measured: 2048-step segments 1.566 ms at 32768^2 against 1.60 with 1024, fewer
-        // snapshots; 8192^2 prefers 1024, its last segment's tail is a larger share)
-        pl->seg_len = knobs().dual_seg ? knobs().dual_seg : nlong >= 16384 ? 2048 : 1024;
-        int jmax = 1;
-        for (const StripDesc &sd : pl->strips) jmax = std::max(jmax, (sd.nsteps + pl->seg_len - 1) / pl->seg_len);
-        pl->seg_stride = jmax;
-        // tasks in the order their data appears: strip k (of its pair) reaches segment j after about
-        // k hand-off lags (~112 steps) plus (j + 1) segments, so the key is k + D (j + 1), D = seg / 112
-        const int D = std::max(1, pl->seg_len / 112);
-        int64_t dmax = 0;
-        for (const PairDesc &d : pl->pairs)
-            if (d.num_strips > 0)
-                dmax = std::max<int64_t>(dmax, d.num_strips - 1 + (int64_t)D * ((pl->strips[d.first_strip].nsteps + pl->seg_len - 1) / pl->seg_len));
-        for (int64_t key = 0; key <= dmax; ++key)
+        bool band = knobs().band != 0 && pl->R == 1 && pl->sk == kArr8 && pl->chain && pl->W % 2 == 0;
+        for (const PairDesc &d : pl->pairs) band = band && (d.num_strips == 0 || d.first_strip % 2 == 0);
+        int64_t nb = 0;
+        for (const PairDesc &d : pl->pairs) nb += std::max(0, (d.num_strips + 1) / 2 - 1);
+        const int64_t stripGroups = ((int64_t)pl->strips.size() + pl->W - 1) / pl->W;
+        const int64_t bandGroups = (nb + pl->W - 1) / pl->W;
+        band = band && nb > 0 && stripGroups + bandGroups <= pl->num_cu;
+        if (band)
+        {
+            // bands b = 0 .. B-2 of each pair (B = ceil(strips / 2); the last band's bottom row feeds
+            // nothing); every band publishes its bottom row to granules. The strips keep their planes;
+            // a strip at a group start takes its feed from the granules of the band above, the others
+            // from the strip above through the group's rings, and a group's last strip publishes nothing.
+            granules = 0;
             for (const PairDesc &d : pl->pairs)
             {
-                if (d.num_strips == 0) continue;
-                const int J = (pl->strips[d.first_strip].nsteps + pl->seg_len - 1) / pl->seg_len;
-                for (int jj = 0; jj < J; ++jj)
+                const uint64_t n = d.text_len;
+                const int B = (d.num_strips + 1) / 2;
+                const int64_t fb = (int64_t)pl->bands.size();
+                for (int b = 0; b + 1 < B; ++b)
                 {
-                    const int64_t k = key - (int64_t)D * (jj + 1);
-                    if (k >= 0 && k < d.num_strips)
-                    {
-                        pl->h_tasks.push_back(d.first_strip + (int32_t)k);
-                        pl->h_tasks.push_back(jj);
-                    }
+                    StripDesc bd = pl->strips[d.first_strip + 2 * b];
+                    bd.row0 = 1 + b * 2 * kWave;
+                    bd.flags = (b > 0 ? kHasPrev : 0) | kHasNext;
+                    bd.mask_off = 0;
+                    bd.bnd_in = b > 0 ? pl->bands.back().bnd_out : 0;
+                    bd.bnd_out = granules;
+                    granules += n + 8;
+                    pl->bands.push_back(bd);
+                }
+                for (int k = 0; k < d.num_strips; ++k)
+                {
+                    StripDesc &sd = pl->strips[d.first_strip + k];
+                    const int i = d.first_strip + k;
+                    if (k + 1 < d.num_strips && (i + 1) % pl->W == 0) sd.flags &= ~kHasNext;
+                    sd.bnd_out = 0;
+                    sd.bnd_in = (k > 0 && i % pl->W == 0) ? pl->bands[fb + k / 2 - 1].bnd_out : 0;
                 }
             }
+            pl->band = true;
+        }
     }
 
     // ---- tables ----
@@ -826,7 +812,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_strips, sizeof(StripDesc) * nstr},
         {(void **)&pl->d_prof, sizeof(int32_t) * 4},
         {(void **)&pl->d_table, sizeof(int32_t) * A * A},
-        {(void **)&pl->d_tasks, sizeof(int32_t) * pl->h_tasks.size()},
+        {(void **)&pl->d_bands, sizeof(StripDesc) * pl->bands.size()},
         {(void **)&pl->d_ws_text, in ? inN + 16 : 0},
         {(void **)&pl->d_ws_pattern, in ? inM + 16 : 0},
         {(void **)&pl->d_ctrl, sizeof(Control)},
@@ -836,7 +822,6 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_codes, codeB},
         // (+8 KiB: the traceback's plane prefetch may read a few chunks past a strip)
         {(void **)&pl->d_masks, pl->bytes_masks + 8192},
-        {(void **)&pl->d_snap, pl->dual ? sizeof(uint64_t) * 2 * kWave * pl->strips.size() * pl->seg_stride : 0},
         {(void **)&pl->d_bnd, ws ? 0 : bndB},  // (workspace plans: the context's granule buffer)
         {(void **)&pl->d_best, bestB},
         {(void **)&pl->d_score, sizeof(int32_t) * npp},
@@ -879,7 +864,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         put(pl->d_strips, pl->strips.data(), sizeof(StripDesc) * pl->strips.size());
         put(pl->d_prof, prof.data(), sizeof(int32_t) * 4);
         put(pl->d_table, table.data(), sizeof(int32_t) * A * A);
-        put(pl->d_tasks, pl->h_tasks.data(), sizeof(int32_t) * pl->h_tasks.size());
+        put(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size());
         put(pl->d_ws_text, in->text, inN);
         put(pl->d_ws_pattern, in->pattern, inM);
         std::memset(h + ((char *)pl->d_ctrl - pl->d_up), 0, sizeof(Control));
@@ -906,9 +891,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemcpyAsync(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(pl->d_bnd, 0, bndB, st) == hipSuccess &&
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
-    if (okc && pl->dual)
-        okc = hipMemcpyAsync(pl->d_tasks, pl->h_tasks.data(), sizeof(int32_t) * pl->h_tasks.size(), hipMemcpyHostToDevice, st) == hipSuccess &&
-              hipMemsetAsync(pl->d_snap, 0, sizeof(uint64_t) * 2 * kWave * pl->strips.size() * pl->seg_stride, st) == hipSuccess;
+    if (okc && pl->band)
+        okc = hipMemcpyAsync(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size(), hipMemcpyHostToDevice, st) == hipSuccess;
     // a plan of its own is complete when sa_plan_create returns (callers fill on other streams)
     if (okc) okc = hipStreamSynchronize(st) == hipSuccess;
     if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
@@ -985,20 +969,17 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.timeout_ticks = (uint64_t)(knobs().handoff_timeout_s * 1e8);
         a.io_sleep = knobs().io_sleep;
         a.chain_lds = knobs().chain_lds_kb * 1024;
-        a.dual = 0;
-        a.score_wgs = 0;
-        a.seg_len = pl->seg_len;
-        a.seg_stride = pl->seg_stride;
-        a.num_dir_tasks = (int32_t)(pl->h_tasks.size() / 2);
-        a.dir_tasks = pl->d_tasks;
-        a.snap = pl->d_snap;
+        a.bands = pl->d_bands;
+        a.num_bands = 0;
+        a.num_band_groups = 0;
+        a.band_wgs = 0;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;
         DevPtr<uint64_t> tlBuf;
         if (tlPath)
         {
-            HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * kTimelineWords * ns));
+            HIP_TRY(hipMalloc((void **)&a.timeline, sizeof(uint64_t) * kTimelineWords * (ns + pl->bands.size())));
             tlBuf.reset(a.timeline);
         }
         // (the pair-packed kernel always runs kPairWaves waves per workgroup)
@@ -1015,27 +996,22 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             a.num_groups = (units + W - 1) / W;
             grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
         }
-        if (pl->dual)
+        if (pl->band)
         {
-            // strip groups on the first workgroups, direction workers on the rest, one workgroup per
-            // CU (the LDS request is above half a CU's), so no CU runs a score wave and a direction
-            // wave side by side
-            a.dual = 1;
-            a.score_wgs = a.num_groups;
+            // band groups on the first workgroups, strip groups on the rest, one workgroup per CU (the
+            // LDS request is above half a CU's) and every group in flight at once (plan_create checked
+            // that they fit): a strip group waits only for bands, which never wait for strips
+            a.num_bands = (int32_t)pl->bands.size();
+            a.num_band_groups = (a.num_bands + W - 1) / W;
+            a.band_wgs = a.num_band_groups;
             a.chain_lds = std::max(a.chain_lds, 96 * 1024);
-            grid = std::max(a.num_groups + 1, pl->num_cu);
+            grid = a.num_band_groups + a.num_groups;
         }
-        if (pl->split)
-        {
-            // one workgroup per CU (its LDS holds the F rings)
-            grid = std::min(a.num_groups, std::max(1, pl->num_cu));
-            launch_fill_split(a, pl->mode == SA_LOCAL, grid, W, st);
-        }
-        else launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
+        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
         HIP_TRY(hipGetLastError());
         if (tlPath)
         {
-            std::vector<uint64_t> tl(kTimelineWords * (size_t)ns);
+            std::vector<uint64_t> tl(kTimelineWords * (ns + pl->bands.size()));
             HIP_TRY(hipStreamSynchronize(st));
             HIP_TRY(hipMemcpy(tl.data(), a.timeline, tl.size() * 8, hipMemcpyDeviceToHost));
             if (FILE *f = std::fopen(tlPath, "wb"))
@@ -1236,6 +1212,17 @@ int sa_plan_info(const sa_plan *pl, int64_t *num_strips, int32_t *rows_per_lane,
 }
 
 const void *sa_plan_device_results(const sa_plan *pl) { return pl ? (const void *)pl->d_results : nullptr; }
+
+int sa_plan_copy_results(const sa_plan *pl, void *d_dst, void *stream)
+{
+    if (!pl || (!d_dst && !pl->pairs.empty())) return fail(SA_ERR_INVALID, "sa_plan_copy_results: null argument");
+    if (pl->pairs.empty()) return SA_OK;
+    DeviceGuard dg(pl->device);
+    if (!dg.ok) return fail(SA_ERR_HIP, "hipSetDevice failed");
+    HIP_TRY(hipMemcpyAsync(d_dst, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToDevice,
+                           (hipStream_t)stream));
+    return SA_OK;
+}
 
 int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *pattern, uint64_t m, int device,
                   sa_result *out, char *at, char *ap, uint64_t cap, double *fill_us)

@@ -34,19 +34,16 @@ struct FillArgs {
     int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
     int32_t chain_lds;          // chain launches: dynamic LDS bytes (>= group_lds_bytes(W); more
                                 // than half a CU's LDS keeps one workgroup per CU)
-    // DUAL fill (R = 1 int8-profile global chains, sa_fill.hip): score waves run the recurrence
-    // alone, publish every bottom row to bnd and snapshot their state every seg_len steps; direction
-    // waves on the other CUs recompute each (strip, segment) from that and write the planes
-    int32_t dual;               // 0: one-wave fill
-    int32_t score_wgs;          // dual: workgroups [0, score_wgs) take strip groups, the rest direction tasks
-    int32_t seg_len;            // dual: steps per segment (a multiple of 64)
-    int32_t seg_stride;         // dual: snapshot entries per strip
-    int32_t num_dir_tasks;
-    const int32_t *dir_tasks;   // dual: {strip, segment} in the order direction waves take them
-    uint64_t *snap;             // dual: per (strip, segment) {value, epoch} of F and diag, 64 lanes each
+    // BAND fill (R = 1 int8-profile chains, sa_fill.hip process_band): 128-row score strips (bands)
+    // run the recurrence alone on workgroups [0, band_wgs) and feed the 64-row strips, which the other
+    // workgroups run in groups of W (the first strip of a group from the band above's granules)
+    const StripDesc *bands;     // the bands (null / num_bands = 0: no band fill)
+    int32_t num_bands;
+    int32_t num_band_groups;    // ceil(num_bands / W)
+    int32_t band_wgs;
 };
 
-constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip (words 6..35: experiment progress stamps)
+constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..35: experiment progress stamps)
 constexpr int kMaxWaves = 4;       // compute waves per chain workgroup (+1 I/O wave: 320 threads; one
                                    // compute wave per SIMD: two per SIMD ran 2.2x slower per step)
 constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed batch kernel
@@ -71,10 +68,6 @@ constexpr bool kIsArr = SK == kArr || SK == kArr8;
 // Fill launch for strip height R (instantiated in fill_r<R>.hip).
 template <int R>
 void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st);
-// SPLIT fill (R = 1, int8 text profiles, global, strip chains): a score wave and a dir wave per strip,
-// W strips per workgroup (1..3); in fill_r1.hip (sa_split.inc).
-void launch_fill_split(const FillArgs &a, bool local, int grid, int W, hipStream_t st);
-size_t split_fill_lds_bytes(int W);
 #ifndef SA_FILL_R
 extern template void launch_fill_r<1>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
 extern template void launch_fill_r<2>(const FillArgs &, bool, int, int, int, bool, hipStream_t);

@@ -87,8 +87,8 @@ constexpr int kRingMask = kRing - 1;
 #endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
-    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_SPLIT_INC) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK) || defined(SA_EXP_DUAL_CSTORE)
+    defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -101,7 +101,7 @@ constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (b
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
     int cons[kMaxWaves + 1];       // cons[w]: columns read from ring[w] (producer backpressure)
-    int drain[kMaxWaves + 1];      // dual: drain[w]: columns of ring[w] the I/O wave has copied to granules
+    int drain[kMaxWaves + 1];      // band fill: drain[w]: columns of ring[w] copied to granules
     int group;                     // group index taken from the queue
     int nwaves;                    // compute waves of the workgroup (W)
 };
@@ -110,16 +110,12 @@ struct GroupHdr {
 // lane's sink slot is its ring slot offset: the publish address is one add per body)
 constexpr int kSink = kRing + kWave;
 __host__ __device__ constexpr size_t group_lds_bytes(int W) { return sizeof(GroupHdr) + ((size_t)(W + 1) * kRing + kSink) * 4; }
-// What a strip's waves see of their workgroup's LDS: the one-wave kernel's GroupHdr, or the split
-// kernel's header and F rings (sa_split.inc)
+// What a strip's waves see of their workgroup's LDS (GroupHdr)
 struct StripLds {
     const int *S;   // generic score table (kTable)
     int *cons;      // cons[w]: columns read from ring[w] (producer backpressure)
     int nwaves;     // strips of the workgroup (W): the shared sink follows ring W
-    int *frings;    // split: the strips' F rings, else null
-    int *dcons;     // split: dcons[w] = steps whose F values the dir wave of strip w has read
-    int *prog;      // split: prog[w] = steps the score wave of strip w has completed (strips without HN)
-    int *drain;     // dual: drain[w] = columns of ring[w] the I/O wave has copied to granules
+    int *drain;     // band fill: drain[w] = columns of ring[w] copied to granules (drain / I/O wave)
 };
 
 // Constant 100 MHz clock, read and waited for in one statement: a compiler-visible s_memrealtime
@@ -207,13 +203,11 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 // below (HN) that shift's `old` is F[R-1], so lane 63 takes in the previous step's bottom-row value:
 // after U steps lanes 64-U..63 of Q hold the bottom row of steps s0-1 .. s0+U-2, and one full-wave
 // ds_write publishes them (the other lanes write a dummy slot). Steps [QB, QE) of the body.
-// SPLIT (R = 1): every step's F also goes to this lane's F-ring row at physical slot (s & 127) + 1
-// (sa_split.inc), byte offset frow in LDS; the direction bits are left to the dir wave.
-template <int R, bool LOCAL, int SK, int KIND, bool HN, int QB, int QE, bool SPLIT = false>
+template <int R, bool LOCAL, int SK, int KIND, bool HN, int QB, int QE>
 __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, int lane, int n, int g,
                                          int kb, const int (&prof)[R], const int (&T)[Codes<R, SK>::NT],
                                          int (&F)[R], int (&best)[R], int &upPrev, int &Q,
-                                         uint32_t (&acc)[3][Cfg<R>::NW], uint32_t frow = 0)
+                                         uint32_t (&acc)[3][Cfg<R>::NW])
 {
     sfor<QE - QB>([&](auto Qc) {
         constexpr int q = QB + decltype(Qc)::value;
@@ -283,7 +277,6 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 else best[rho] = max(best[rho], key);
             }
             if constexpr (RAMP) Fn = act ? Fn : left;
-            if constexpr (SPLIT) asm volatile("ds_write_b32 %0, %1" ::"v"(frow + ((((uint32_t)s & 127u) + 1u) << 2)), "v"(Fn));
             diag = left;
             up = Fn;
             F[rho] = Fn;
@@ -352,60 +345,32 @@ template <bool LOCAL, bool HN, bool HP, int HALF>
 __device__ __forceinline__ void steps_asm(StepRegs &r);
 template <bool LOCAL>
 __device__ __forceinline__ void merge_asm(StepRegs &r);
-template <bool HN, bool HP>
-__device__ __forceinline__ void rec_steps_asm(StepRegs &r);
+// Register state of the band fill's score steps (two rows per lane; sa_fill_steps.inc, generated by
+// tools/gen_fill_asm.py band_block): eight registers rotate with period 8, four carry state across
+// bodies
+struct BandRegs {
+    int Q, diag, F0, F1;  // feed queue, up of the previous step (row 0's diag), rows 0 / 1
+    int TA[4], TB[4];     // text-profile words of the body for row 0 / row 1 (4 steps each)
+    int g;                // local: the gap (H = X - g, saturated at 0)
+    int pfaddr, pf;       // HP: as StepRegs
+    int pubaddr, pubtag, ctag, msb;
+    uint64_t bad;
+};
+template <bool LOCAL, bool HN, bool HP>
+__device__ __forceinline__ void band_steps_asm(BandRegs &r);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_FILL_INC)
 #include SA_EXP_FILL_INC  // tools/gen_fill_asm.py variants (timing ablations)
 #else
 #include "sa_fill_steps.inc"
 #endif
 
-// SPLIT fill (R = 1, int8 text profiles, global; sa_split.inc): each strip has a score wave and a dir
-// wave. The score wave writes every step's F to an LDS F ring: kFRows rows of kFRow dwords per strip,
-// row -1 = the strip's feed (lane 0's `up`) at slot (step & 127), row 1 + k = lane k's F at physical
-// slot (step & 127) + 1 (a body's 16 values are one run: slots up to 128). 132 dwords = 528 bytes = 16
-// times an odd number: the dir wave's lane-strided ds_read_b128 are conflict-free.
-constexpr int kFRow = 132;
-constexpr int kFRows = 65;
-constexpr int kMaxSplitW = 3;  // strips per split workgroup: 2 W + 1 waves (<= 7: 448 threads)
-struct ScoreRegs {
-    int Q, Qn, diag, F;
-    int T[4];
-    uint32_t fra;          // this lane's F-ring row + (s0 & 96) * 4 (the body's writes are offsets)
-    int pfaddr, pf;        // HP: as StepRegs
-    int pubaddr, pubtag, ctag, msb;
-    uint64_t bad;
-    uint32_t dcaddr;       // DC: LDS address of the dir wave's consumption word
-    int dcv;               // DC: its value, read during the block
-};
-struct DirRegs {
-    int O[16], U[16];      // O[i] = F_{s0+i-1} (i >= 1), U[i] = the lane above's F_{s0+i-1} / the feed
-    int oc, ex;            // F_{s0-1} (carried), F_{s0+15}
-    int X[8], Y[8];        // direction differences, one byte per step (as StepRegs)
-    int mk[8];
-    uint32_t acc0, acc1;
-};
-template <bool HN, bool HP, int HALF, bool DC>
-__device__ __forceinline__ void score_asm(ScoreRegs &r);
-template <int HALF>
-__device__ __forceinline__ void dir_asm(DirRegs &r);
-#if SA_FILL_R == 1
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_SPLIT_INC)
-#include SA_EXP_SPLIT_INC  // tools/gen_split_asm.py variants (timing ablations)
-#else
-#include "sa_split_steps.inc"
-#endif
-#endif
-
 // One strip. HP / HN: the strip has a strip above (feeds from rin) / below (publishes into rout);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
 // kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
-template <int R, bool LOCAL, int SK, bool HP, bool HN, bool SPLIT = false, bool DUALS = false>
+template <int R, bool LOCAL, int SK, bool HP, bool HN>
 __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
-    static_assert(!SPLIT || (R == 1 && SK == kArr8 && !LOCAL), "the split fill is R = 1, int8 profiles, global");
-    static_assert(!DUALS || (R == 1 && SK == kArr8 && !LOCAL && !SPLIT), "the dual fill is R = 1, int8 profiles, global");
     constexpr int U = Cfg<R>::U;
     constexpr int NT = Codes<R, SK>::NT;
     // Descriptors come in through vector loads (the kernel stores to global memory, so the compiler
@@ -644,43 +609,12 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
                     ++dbgPubSpins;
 #endif
                     consKnown = uniform(lds_ld(consOut));
-                    // dual: the I/O wave copies this ring to granules too and must have read a slot
-#if !(defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE))
-                    if constexpr (DUALS) consKnown = min(consKnown, uniform(lds_ld((lds_int *)&L.drain[w + 1])));
-#endif
                     if (cLast - kRing <= consKnown) break;
                     __builtin_amdgcn_s_sleep(1);
                     if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
                 }
             }
         }
-    };
-    // DUAL score wave: every seg_len steps its state (F of the step before, diag) goes to the strip's
-    // snapshot entry (its bottom row reaches the granules through the I/O wave, io_wave)
-    const uint32_t epochv = a.epoch;
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
-    // experiment: the compute wave stores its published bottom rows to its granules itself
-    const __amdgpu_buffer_rsrc_t brsrc =
-        __builtin_amdgcn_make_buffer_rsrc(a.bnd + (DUALS && HN ? sd.bnd_out : 0), 0, (int)(8 * pd.text_len), kBufRsrcWord3);
-    const uint32_t browOff = lane >= kWave - U ? (uint32_t)(lane - (kWave - U)) * 8u : 0x80000000u;
-#endif
-    auto brow_store = [&](int s0, int qv) __attribute__((always_inline)) {
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
-        if constexpr (DUALS && HN)
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(uint32_t)qv, epochv}, brsrc, browOff + (uint32_t)(s0 - 64) * 8u, 0, kAuxSc1);
-#else
-        (void)s0;
-        (void)qv;
-#endif
-    };
-    auto snapshot = [&](int s0, int f, int dg) __attribute__((always_inline)) {
-        if constexpr (DUALS)
-            if (s0 > 0 && (s0 & (a.seg_len - 1)) == 0)  // (seg_len: a power of two)
-            {
-                uint64_t *e = a.snap + ((size_t)idx * a.seg_stride + (uint32_t)s0 / (uint32_t)a.seg_len) * (2 * kWave) + lane;
-                __hip_atomic_store(e, ((uint64_t)epochv << 32) | (uint32_t)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(e + kWave, ((uint64_t)epochv << 32) | (uint32_t)dg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
     };
     auto publish = [&](int s0) __attribute__((always_inline)) {
         if constexpr (HN)
@@ -691,44 +625,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     };
     int msbv;  // one VGPR for the strip (the compiler would rematerialize a literal per body)
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
-    // SPLIT: this lane's F-ring row, where its Q lane goes (lanes 0..15: the feed row -1; others: the
-    // sink), the dir wave's consumption word, and (strips without HN) the progress word
-    uint32_t frowOff = 0, feedOff = 0, progOff = 0;
-    int dKnown = 0;  // steps the dir wave is known to have consumed
-    uint32_t dWaits = 0;  // timeline: bodies that waited for the dir wave
-    if constexpr (SPLIT)
-    {
-        int *fr = L.frings + w * kFRows * kFRow;
-        frowOff = lds_off((lds_int *)(fr + (1 + lane) * kFRow));
-        const lds_int *sink = rings + (L.nwaves + 1) * kRing;
-        feedOff = lane < U ? lds_off((lds_int *)(fr + lane)) : lds_off(sink + lane);
-        progOff = lane == 0 ? lds_off((lds_int *)&L.prog[w]) : lds_off(sink + lane);
-    }
-    // F ring backpressure: a body at s0 overwrites the slots of steps s0 - 128 .. s0 - 113, which
-    // the dir wave has read once it has consumed s0 - 112
-    auto dcons_wait = [&](int need) __attribute__((always_inline)) {
-        if constexpr (SPLIT)
-        {
-            const uint64_t t0 = now_ticks();
-            ++dWaits;
-            for (uint32_t spin = 1;; ++spin)
-            {
-                dKnown = uniform(ds_read_sync((lds_int *)&L.dcons[w]));
-                if (dKnown >= need) break;
-                __builtin_amdgcn_s_sleep(1);
-                if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
-            }
-        }
-    };
-    auto split_pre = [&](int s0) __attribute__((always_inline)) {
-        // the feed (Q lanes 0..15) -> row -1, slot (s0 & 127) + lane: the dir wave's lane-0 `up`
-        if constexpr (SPLIT) asm volatile("ds_write_b32 %0, %1" ::"v"(feedOff + (uint32_t)((s0 & 127) * 4)), "v"(Q));
-    };
-    auto split_post = [&](int s0) __attribute__((always_inline)) {
-        // strips without HN tell their dir wave through the progress word (with HN it polls the
-        // published bottom row)
-        if constexpr (SPLIT && !HN) asm volatile("ds_write_b32 %0, %1" ::"v"(progOff), "v"(s0 + U));
-    };
     // the asm bodies' direction-difference bytes (kept across the two bodies of a plane word) and the
     // merge masks 0x80808080 >> g (opaque: built once per strip, not rematerialized per word)
     int dX[8], dY[8], dZ[8], mkv[8], mzv[4];
@@ -781,58 +677,19 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         }
 #endif
         load_codes(s0 + kAhead * U, Tn);
-        snapshot(s0, F[0], upPrev);
-        if constexpr (SPLIT && kAsm && KIND == kSteady)
-        {
-            constexpr int HALF = POS & 1;
-            constexpr bool DC = HALF == 0;  // one consumption read per body pair
-            ScoreRegs r;
-            split_pre(s0);
-            r.Q = Q;
-            r.diag = upPrev;
-            r.F = F[0];
-            sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
-            r.fra = frowOff + (uint32_t)((s0 & 96) * 4);
-            r.pfaddr = HP ? (int)(rinLaneOff + 4u * (uint32_t)ring_slot(s1 + 1)) : 0;
-            r.ctag = ring_tag_raw(s1 + 1);
-            r.msb = msbv;
-            if constexpr (POS == 0) pub_wait(s0 + 3 * U);
-            else if constexpr (POS == 2) pub_wait(s0 + U);
-            r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
-            r.pubtag = ring_tag_raw(s0 - 63);
-            r.dcaddr = lds_off((lds_int *)&L.dcons[w]);
-            score_asm<HN, HP, HALF, DC>(r);
-            if constexpr (HP)
-            {
-                pfVal = r.pf;
-                pfBad = r.bad;
-                pfTagged = true;
-            }
-            Q = r.Q;
-            upPrev = r.diag;
-            F[0] = r.F;
-            split_post(s0);
-            if constexpr (DC)
-            {
-                // the next pair (s0 + 32, s0 + 48) needs the dir wave at s0 + 48 - 112
-                dKnown = uniform(r.dcv);
-                if (__builtin_expect(s0 - 64 > dKnown, 0)) dcons_wait(s0 - 64);
-            }
-        }
-        else if constexpr (kAsm && KIND == kSteady)
+        if constexpr (kAsm && KIND == kSteady)
         {
             static_assert(U == 16 && NT == 4, "sa_fill_steps.inc is generated for these");
             StepRegs r;
             r.Q = Q;
             r.diag = upPrev;
             r.F = F[0];
-            if constexpr (!DUALS)
-                sfor<8>([&](auto Gc) {
-                    constexpr int g = decltype(Gc)::value;
-                    r.X[g] = dX[g];
-                    r.Y[g] = dY[g];
-                    if constexpr (LOCAL) r.Z[g] = dZ[g];
-                });
+            sfor<8>([&](auto Gc) {
+                constexpr int g = decltype(Gc)::value;
+                r.X[g] = dX[g];
+                r.Y[g] = dY[g];
+                if constexpr (LOCAL) r.Z[g] = dZ[g];
+            });
             r.bm = -16;  // below every (H << kb) - q
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
             r.g = g;
@@ -847,8 +704,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             else if constexpr (POS == 2) pub_wait(s0 + U);
             r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
             r.pubtag = ring_tag_raw(s0 - 63);
-            if constexpr (DUALS) rec_steps_asm<HN, HP>(r);  // the recurrence alone (direction waves)
-            else steps_asm<LOCAL, HN, HP, POS & 1>(r);  // with HP: reads the next body's feed after step 12
+            steps_asm<LOCAL, HN, HP, POS & 1>(r);  // with HP: reads the next body's feed after step 12
             if constexpr (HP)
             {
                 pfVal = r.pf;
@@ -858,15 +714,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             Q = r.Q;
             upPrev = r.diag;
             F[0] = r.F;
-            if constexpr (DUALS) brow_store(s0, r.Qn);
-            if constexpr (!DUALS)
-                sfor<8>([&](auto Gc) {
-                    constexpr int g = decltype(Gc)::value;
-                    dX[g] = r.X[g];
-                    dY[g] = r.Y[g];
-                    if constexpr (LOCAL) dZ[g] = r.Z[g];
-                });
-            if constexpr ((POS & 1) == 1 && !DUALS)
+            sfor<8>([&](auto Gc) {
+                constexpr int g = decltype(Gc)::value;
+                dX[g] = r.X[g];
+                dY[g] = r.Y[g];
+                if constexpr (LOCAL) dZ[g] = r.Z[g];
+            });
+            if constexpr ((POS & 1) == 1)
             {
                 // the chunk's second body: its bits into the two interleaved words for the store below
                 sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
@@ -889,22 +743,16 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         }
         else
         {
-            if constexpr (SPLIT)
-            {
-                if (s0 - 112 > dKnown) dcons_wait(s0 - 112);
-                split_pre(s0);
-            }
-            run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead, SPLIT>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc, frowOff);
+            run_body<R, LOCAL, SK, KIND, HN, 0, U - kPfLead>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
             prefetch(s1);
-            run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U, SPLIT>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc, frowOff);
+            run_body<R, LOCAL, SK, KIND, HN, U - kPfLead, U>(L.S, s0, lane, n, g, kb, prof, T, F, best, upPrev, Q, acc);
             // R = 1: a body fills one interleaved word; the chunk's first word waits in acc[1][0]
             if constexpr (R == 1 && !second::value) acc[1][0] = acc[0][0];
-            split_post(s0);
         }
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STORE)
         if constexpr (false)  // timing ablation: no direction planes are written
 #else
-        if constexpr (!SPLIT && !DUALS && (Cfg<R>::BPC == 1 || second::value))
+        if constexpr (Cfg<R>::BPC == 1 || second::value)
 #endif
         {
             const int chunk = (int)((uint32_t)(s1 * R) / Cfg<R>::CS) - 1;
@@ -1029,7 +877,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         tl[41] = dbgFeedSpinsSteady;
 #endif
         tl[5] = __builtin_amdgcn_s_memtime();
-        if constexpr (SPLIT) tl[45] = dWaits;
         // XCC_ID (hwreg 20) and HW_ID (hwreg 4: wave, SIMD, CU, SE fields)
         tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
                 (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
@@ -1051,6 +898,247 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
             });
             a.pair_score[sd.pair] = v - g * (m + n);
         }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// BAND fill (R = 1 int8 text-profile chains): score strips of two rows per lane
+// ------------------------------------------------------------------------------------------------
+// A chain of 64-row strips hands its bottom row down once per 64 rows, and every hand-off costs the
+// 64-step lane skew plus the hand-off latency: at 32768^2 that ramp (511 hand-offs) was two thirds of
+// the fill. A BAND is a 128-row score strip: lane k owns rows row0 + 2k and row0 + 2k + 1 and works on
+// column s - k + 1 at step s for both, so a band covers twice the rows per lane skew, and the chain of
+// bands has half the hand-offs. Its recurrence runs alone (band_steps_asm: 6 VALU per step, 8 local,
+// no direction bits, no best-cell keys); its bottom row, published with the same step <-> column map,
+// ring tags and granules as a 64-row strip, feeds the next band and, through the granules (drain and
+// I/O waves), the 64-row strips of the band below. Those strips (process_strip, the one-wave kernel)
+// run in groups of W on the other workgroups: the group's first strip is fed from the band above's
+// granules, the rest through the group's LDS rings, and they write the direction planes, the global
+// score and the local best cells exactly as the one-wave fill does (the same integer operations on
+// the same inputs). Bands exist for every band of a pair but its last (whose bottom row feeds
+// nothing) and need no final state; the local recurrence saturates H = X - g at 0 with one clamped
+// subtract (g >= 0, X >= 0), so local is banded as well.
+template <bool LOCAL, bool HP, bool HN>
+__device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
+{
+    constexpr int U = 16;
+    typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
+    idx = uniform(idx);
+    StripDesc sd = a.bands[idx];
+    sd.pair = uniform(sd.pair);
+    sd.row0 = uniform(sd.row0);
+    sd.nsteps = uniform(sd.nsteps);
+    PairDesc pd = a.pairs[sd.pair];
+    pd.text_len = uniform64(pd.text_len);
+    pd.pattern_len = uniform64(pd.pattern_len);
+    pd.pattern_off = uniform64(pd.pattern_off);
+    pd.code_off = uniform64(pd.code_off);
+    pd.code_len = uniform64(pd.code_len);
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
+    // the lane's two rows: byte copy k % 4 of each row letter's text profile (process_strip, kArr8)
+    uint32_t coff[2];
+    sfor<2>([&](auto Rc) {
+        constexpr int rho = decltype(Rc)::value;
+        const int i = sd.row0 + 2 * lane + rho;
+        int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
+        c = min(max(c, 0), a.A - 1);
+        coff[rho] = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+    });
+    const __amdgpu_buffer_rsrc_t crsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
+    auto load_codes = [&](int s0, int (&dA)[4], int (&dB)[4]) __attribute__((always_inline)) {
+        const i32x4u va = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[0], s0, 0);
+        const i32x4u vb = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[1], s0, 0);
+        dA[0] = va.x;
+        dA[1] = va.y;
+        dA[2] = va.z;
+        dA[3] = va.w;
+        dB[0] = vb.x;
+        dB[1] = vb.y;
+        dB[2] = vb.z;
+        dB[3] = vb.w;
+    };
+    lds_int *rin = (lds_int *)(rings + w * kRing);
+    lds_int *rout = (lds_int *)(rings + (w + 1) * kRing);
+    lds_int *consIn = (lds_int *)&L.cons[w];
+    lds_int *consOut = (lds_int *)&L.cons[w + 1];
+    lds_int *drainOut = (lds_int *)&L.drain[w + 1];
+    lds_int *sink = rings + (L.nwaves + 1) * kRing;
+    lds_int *pubBase = lane >= kWave - U ? rout + (lane - (kWave - U)) : sink + lane;
+    const uint32_t rinLaneOff = lds_off(rin + lane);
+    // the feed protocol of process_strip: read after step BAND_PF_STEP, tags checked at the body end
+    int Q = 0, diag = 0, F0 = 0, F1 = 0;  // column-0 boundary
+    int pfVal = 0;
+    bool pfTagged = false;
+    uint64_t pfBad = 0;
+    auto feed = [&](int base, bool full) __attribute__((always_inline)) {
+        if constexpr (!HP)
+        {
+            asm volatile("v_mov_b32 %0, 0" : "=v"(Q));  // row 0 boundary (opaque: see process_strip)
+            return;
+        }
+        else
+        {
+            const int tag = ring_tag(base + 1);
+            uint64_t need = (1ull << U) - 1;
+            if (!full)
+            {
+                int cnt;
+                asm("s_sub_i32 %1, %2, %3\n\ts_max_i32 %1, %1, 0\n\ts_min_i32 %1, %1, %4\n\ts_bfm_b64 %0, %1, 0"
+                    : "=s"(need), "=&s"(cnt)
+                    : "s"(n), "s"(base), "i"(U)
+                    : "scc");
+            }
+            int x = pfTagged ? pfVal : pfVal ^ tag;
+            const uint64_t bad = pfTagged ? pfBad : (ballot(x < 0) & ((1ull << U) - 1));
+            pfTagged = false;
+            if (__builtin_expect((full ? bad : (bad & need)) != 0, 0))
+            {
+                uint64_t t0 = 0;
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    if (spin > 16) __builtin_amdgcn_s_sleep(1);
+                    x = ds_read_sync(rin + lane + ring_slot(base + 1)) ^ tag;
+                    if ((ballot(x < 0) & need) == 0) break;
+                    if ((spin & 255) == 0)
+                    {
+                        if (t0 == 0) t0 = now_ticks();
+                        else if (!keep_waiting(a, t0, lane)) break;
+                    }
+                }
+            }
+            Q = x;
+        }
+    };
+    const uint32_t consAddr = lane == 0 ? lds_off(consIn) : lds_off(sink + lane);
+    auto consumed = [&](int upto) __attribute__((always_inline)) {
+        if constexpr (HP) asm volatile("ds_write_b32 %0, %1" ::"v"(consAddr), "v"(upto));
+    };
+    // a ring slot is reused once the drain or I/O wave (drain) and the next band (cons) have read it;
+    // a next band of the group that starts another pair's chain reads nothing (the I/O wave, which
+    // drains the group's last ring, keeps cons too)
+    const bool nextReads = !(w + 1 < L.nwaves && idx + 1 < a.num_bands) || (uniform(a.bands[idx + 1].flags) & kHasPrev);
+    int consKnown = 0;
+    auto pub_wait = [&](int s0) __attribute__((always_inline)) {
+        if constexpr (HN)
+        {
+            const int cLast = s0 - 64 + U;
+            if (__builtin_expect(cLast - kRing > consKnown, 0))
+            {
+                const uint64_t t0 = now_ticks();
+                for (uint32_t spin = 1;; ++spin)
+                {
+                    consKnown = uniform(lds_ld(drainOut));
+                    if (nextReads) consKnown = min(consKnown, uniform(lds_ld(consOut)));
+                    if (cLast - kRing <= consKnown) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    if ((spin & 255) == 0 && !keep_waiting(a, t0, lane)) break;
+                }
+            }
+        }
+    };
+    int msbv;
+    asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
+    const uint64_t tStart = a.timeline ? now_ticks() : 0;
+    int TA0[4], TA1[4], TB0[4], TB1[4], TC0[4], TC1[4], TD0[4], TD1[4];
+    load_codes(0, TA0, TA1);
+    load_codes(U, TB0, TB1);
+    if constexpr (HP)
+    {
+        int c = 1 + lane;
+        asm volatile("" : "+v"(c));
+        pfVal = lds_ld(rin + ring_slot(c));
+    }
+    feed(0, false);
+    const uint64_t tFed = a.timeline ? now_ticks() : 0;
+    const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
+    uint32_t quadPf = 0;
+    auto set_quad = [&](int s0q) __attribute__((always_inline)) {
+        quadPf = 4u * (uint32_t)s0q + 4u * (U + 64);
+        asm volatile("" : "+s"(quadPf));
+    };
+    auto body = [&](auto pos, auto full, int s0, int (&T0)[4], int (&T1)[4], int (&Tn0)[4], int (&Tn1)[4]) __attribute__((always_inline)) {
+        constexpr int POS = decltype(pos)::value;
+        constexpr bool FULL = decltype(full)::value;
+        const int s1 = s0 + U;
+        load_codes(s0 + 2 * U, Tn0, Tn1);
+        BandRegs r;
+        r.Q = Q;
+        r.diag = diag;
+        r.F0 = F0;
+        r.F1 = F1;
+        sfor<4>([&](auto Wc) {
+            constexpr int q = decltype(Wc)::value;
+            r.TA[q] = T0[q];
+            r.TB[q] = T1[q];
+        });
+        r.g = a.gap;
+        r.pfaddr = HP ? (int)(rinLaneOff + ((quadPf + 4u * U * POS) & (4u * kRingMask))) : 0;
+        r.ctag = ring_tag_raw(s1 + 1);
+        r.msb = msbv;
+        if constexpr (POS == 0) pub_wait(s0 + 3 * U);
+        else if constexpr (POS == 2) pub_wait(s0 + U);
+        r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
+        r.pubtag = ring_tag_raw(s0 - 63);
+        band_steps_asm<LOCAL, HN, HP>(r);
+        if constexpr (HP)
+        {
+            pfVal = r.pf;
+            pfBad = r.bad;
+            pfTagged = true;
+        }
+        Q = r.Q;
+        diag = r.diag;
+        F0 = r.F0;
+        F1 = r.F1;
+        feed(s1, FULL);
+        if constexpr (POS == 3) consumed(s1 + U);
+    };
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    const int nSteps = sd.nsteps;  // a multiple of 2U
+    int s0 = 0;
+    // quads of bodies up to `end` (a multiple of 2U), then at most one pair (process_strip's phases)
+    auto phase = [&](auto full, int end) __attribute__((always_inline)) {
+        for (; s0 + 2 * U < end; s0 += 4 * U)
+        {
+            set_quad(s0);
+            body(P0{}, full, s0, TA0, TA1, TC0, TC1);
+            body(P1{}, full, s0 + U, TB0, TB1, TD0, TD1);
+            body(P2{}, full, s0 + 2 * U, TC0, TC1, TA0, TA1);
+            body(P3{}, full, s0 + 3 * U, TD0, TD1, TB0, TB1);
+        }
+        if (s0 < end)
+        {
+            set_quad(s0 - 2 * U);
+            body(P2{}, full, s0, TA0, TA1, TC0, TC1);
+            body(P3{}, full, s0 + U, TB0, TB1, TD0, TD1);
+            s0 += 2 * U;
+            sfor<4>([&](auto Qc) {
+                constexpr int q = decltype(Qc)::value;
+                TA0[q] = TC0[q];
+                TA1[q] = TC1[q];
+                TB0[q] = TD0[q];
+                TB1[q] = TD1[q];
+            });
+        }
+    };
+    // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered), then the rest
+    phase(std::true_type{}, min(nSteps, max(0, (n - U) / (2 * U) * (2 * U))));
+    phase(std::false_type{}, nSteps);
+    if (a.timeline && lane == 0)
+    {
+        // band records follow the strips' (kTimelineWords words each)
+        uint64_t *tl = a.timeline + kTimelineWords * ((size_t)a.num_strips + idx);
+        tl[0] = tStart;
+        tl[1] = tFed;
+        tl[2] = now_ticks();
+        tl[4] = cFed;
+        tl[5] = __builtin_amdgcn_s_memtime();
+        tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
     }
 }
 
@@ -1253,12 +1341,14 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
 // granules while nothing is there (8 bytes per poll: up to a few hundred waiting groups must not
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
-__device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain, lds_int *rings, int grp, int W, int lane)
+// (strips: the launch's strips, or its bands in a band workgroup)
+__device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *strips, int nstrips, int *cons, int *drain,
+                                        lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
-    const int last = min(first + W, a.num_strips) - 1;
-    const StripDesc sf = a.strips[first];
-    const StripDesc sl = a.strips[last];
+    const int last = min(first + W, nstrips) - 1;
+    const StripDesc sf = strips[first];
+    const StripDesc sl = strips[last];
     const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
     const int nOut = (sl.flags & kHasNext) ? (int)a.pairs[sl.pair].text_len : 0;
     const int wl = last - first + 1;  // ring fed by the last strip
@@ -1311,7 +1401,7 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain
             if (lane == 0)
             {
                 lds_st(consL, drained);
-                lds_st((lds_int *)&drain[wl], drained);  // (dual: the producer waits for min(cons, drain))
+                lds_st((lds_int *)&drain[wl], drained);  // (bands wait for min(cons, drain))
             }
             moved = true;
             if (!full) break;
@@ -1365,203 +1455,16 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, int *cons, int *drain
 }
 
 
-// ------------------------------------------------------------------------------------------------
-// DUAL fill, direction waves (R = 1, int8 text profiles, global, strip chains)
-// ------------------------------------------------------------------------------------------------
-// The strips' score waves run the recurrence alone (rec_steps_asm: 4 VALU per step instead of 7 plus
-// the bit merge), which shortens the chain's critical path; their direction planes are recomputed
-// by direction waves on the workgroups that hold no strip group. A direction task is a segment of
-// seg_len steps of one strip: its state at the segment's first step (F of the step before and the
-// diag register, the score wave's snapshot) and the strip above's bottom row (granules, written by
-// its score wave as it publishes) determine every cell of the segment, so the one-wave kernel's
-// steady bodies (sa_fill_steps.inc, no feed read, no publish) reproduce the score wave's values bit
-// for bit and write the same planes. Snapshots and granules carry the call's epoch: a task polls
-// until its data is there (no flags, no fences), and gives up like every other wait.
-__device__ __forceinline__ bool dir_poll_ok(const FillArgs &a, uint64_t &t0, uint32_t spin, int lane)
-{
-    // (data a few hundred clocks away is re-read at once; a task waiting for its strip to arrive polls
-    // about once a microsecond, so idle direction waves load the memory system little)
-    if (spin > 32) __builtin_amdgcn_s_sleep(32);
-    else if (spin > 8) __builtin_amdgcn_s_sleep(2);
-    if ((spin & 255) == 0)
-    {
-        if (t0 == 0) t0 = now_ticks();
-        else if (!keep_waiting(a, t0, lane)) return false;
-    }
-    return true;
-}
-
-template <bool HP>
-__device__ void process_dir(const FillArgs &a, int idx, int j, int lane)
-{
-    constexpr int U = 16;
-    StripDesc sd = a.strips[idx];
-    sd.pair = uniform(sd.pair);
-    sd.row0 = uniform(sd.row0);
-    sd.nsteps = uniform(sd.nsteps);
-    sd.mask_off = uniform64(sd.mask_off);
-    sd.bnd_in = uniform64(sd.bnd_in);
-    PairDesc pd = a.pairs[sd.pair];
-    pd.text_len = uniform64(pd.text_len);
-    pd.pattern_len = uniform64(pd.pattern_len);
-    pd.pattern_off = uniform64(pd.pattern_off);
-    pd.code_off = uniform64(pd.code_off);
-    pd.code_len = uniform64(pd.code_len);
-    const int n = (int)pd.text_len, m = (int)pd.pattern_len;
-    const int sBeg = j * a.seg_len, sEnd = min(sBeg + a.seg_len, sd.nsteps);
-    const uint32_t epoch = a.epoch;
-    // the lane's text profile (process_strip, kArr8) and plane chunk offset
-    const int row = sd.row0 + lane;
-    int c = row <= m ? (int)a.pattern[pd.pattern_off + row - 1] : 0;
-    c = min(max(c, 0), a.A - 1);
-    const uint32_t coff = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
-    const __amdgpu_buffer_rsrc_t crsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
-    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(a.masks + sd.mask_off * 4, 0, 0x7ffffff0, kBufRsrcWord3);
-    const uint32_t moff = (uint32_t)(lane * Cfg<1>::LW * 4);
-    typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
-    auto load_codes = [&](int s, int (&T)[4]) __attribute__((always_inline)) {
-        const i32x4u v = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff, s, 0);
-        T[0] = v.x;
-        T[1] = v.y;
-        T[2] = v.z;
-        T[3] = v.w;
-    };
-    // feed of the body at s: lanes 0..U-1 = the strip above's bottom row at columns s+1 .. s+U
-    // (granule s + lane); lanes past column n are never needed
-    const uint64_t *fin = a.bnd + sd.bnd_in;
-    const bool feedLane = HP && lane < U;
-    auto feed_load = [&](int s) __attribute__((always_inline)) -> uint64_t {
-        return feedLane && s + lane < n ? load_granule(fin + s + lane) : ((uint64_t)epoch << 32);
-    };
-    uint64_t t0 = 0;
-    bool ok = true;
-    auto feed_take = [&](int s, uint64_t v) __attribute__((always_inline)) -> int {
-        for (uint32_t spin = 1; ok && ballot((uint32_t)(v >> 32) != epoch) != 0; ++spin)
-        {
-            ok = dir_poll_ok(a, t0, spin, lane);
-            v = feed_load(s);
-        }
-        return (int)(uint32_t)v;
-    };
-    // state at sBeg: the column-0 boundary, or the score wave's snapshot
-    int F = 0, diag = 0;
-    if (sBeg > 0)
-    {
-        const uint64_t *e = a.snap + ((size_t)idx * a.seg_stride + j) * (2 * kWave) + lane;
-        for (uint32_t spin = 1; ok; ++spin)
-        {
-            const uint64_t f = load_granule(e), d = load_granule(e + kWave);
-            if (ballot((uint32_t)(f >> 32) != epoch || (uint32_t)(d >> 32) != epoch) == 0)
-            {
-                F = (int)(uint32_t)f;
-                diag = (int)(uint32_t)d;
-                break;
-            }
-            ok = dir_poll_ok(a, t0, spin, lane);
-        }
-    }
-    int mkv[8], dX[8], dY[8];
-    sfor<8>([&](auto Gc) {
-        constexpr int g = decltype(Gc)::value;
-        dX[g] = dY[g] = 0;
-        int mk;
-        asm volatile("v_mov_b32 %0, %1" : "=v"(mk) : "i"((int)(0x80808080u >> g)));
-        mkv[g] = mk;
-    });
-    int TA[4], TB[4], TC[4], TD[4];
-    uint64_t PA = 0, PB = 0, PC = 0, PD = 0;
-    load_codes(sBeg, TA);
-    load_codes(sBeg + U, TB);
-    if constexpr (HP)
-    {
-        PA = feed_load(sBeg);
-        PB = feed_load(sBeg + U);
-    }
-    auto body = [&](auto half, int s, int (&T)[4], uint64_t P) __attribute__((always_inline)) {
-        constexpr int HALF = decltype(half)::value;
-        StepRegs r;
-        if constexpr (HP) r.Q = feed_take(s, P);
-        else asm volatile("v_mov_b32 %0, 0" : "=v"(r.Q));  // row 0 (opaque: see process_strip's feed)
-        r.diag = diag;
-        r.F = F;
-        sfor<8>([&](auto Gc) {
-            constexpr int g = decltype(Gc)::value;
-            r.X[g] = dX[g];
-            r.Y[g] = dY[g];
-        });
-        sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
-        steps_asm<false, false, false, HALF>(r);
-        diag = r.diag;
-        F = r.F;
-        sfor<8>([&](auto Gc) {
-            constexpr int g = decltype(Gc)::value;
-            dX[g] = r.X[g];
-            dY[g] = r.Y[g];
-        });
-        if constexpr (HALF == 1)
-        {
-            sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
-            merge_asm<false>(r);
-            // the chunk of steps s - U .. s + U - 1 (slots 32 * chunk ...)
-            const int chunk = (s + U) / 32 - 1;
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2{r.acc0, r.acc1}, mrsrc, moff, chunk * (kWave * Cfg<1>::LW * 4), 0);
-        }
-    };
-    using H0 = std::integral_constant<int, 0>;
-    using H1 = std::integral_constant<int, 1>;
-    int s = sBeg;
-    for (; s + 2 * U < sEnd; s += 4 * U)
-    {
-        load_codes(s + 2 * U, TC);
-        if constexpr (HP) PC = feed_load(s + 2 * U);
-        body(H0{}, s, TA, PA);
-        load_codes(s + 3 * U, TD);
-        if constexpr (HP) PD = feed_load(s + 3 * U);
-        body(H1{}, s + U, TB, PB);
-        load_codes(s + 4 * U, TA);
-        if constexpr (HP) PA = feed_load(s + 4 * U);
-        body(H0{}, s + 2 * U, TC, PC);
-        load_codes(s + 5 * U, TB);
-        if constexpr (HP) PB = feed_load(s + 5 * U);
-        body(H1{}, s + 3 * U, TD, PD);
-    }
-    if (s < sEnd)
-    {
-        body(H0{}, s, TA, PA);
-        body(H1{}, s + U, TB, PB);
-    }
-}
-
-// Direction workers: every compute wave takes tasks from the list until it is exhausted (or the
-// launch has given up)
-__device__ __forceinline__ void dir_worker(const FillArgs &a, int lane)
-{
-    while (true)
-    {
-        int t = 0;
-        if (lane == 0) t = (int)atomicAdd(&a.ctrl->dir_head, 1u);
-        t = uniform(t);
-        if (t >= a.num_dir_tasks) break;
-        if (__hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
-        const int idx = uniform(a.dir_tasks[2 * t]), j = uniform(a.dir_tasks[2 * t + 1]);
-        if (uniform(a.strips[idx].flags) & kHasPrev) process_dir<true>(a, idx, j, lane);
-        else process_dir<false>(a, idx, j, lane);
-    }
-}
-
-
-// DUAL fill: the drain wave of a score workgroup copies the in-group rings 1 .. wl-1 (fed by strips
-// first .. last-1) to those strips' granules, the direction waves' feed; the I/O wave still drains the
-// last ring. A wave of its own: its write-through stores would otherwise sit in the I/O wave's vmcnt
-// in front of every granule poll (in-order completion) and slow the cross-group hand-off.
+// BAND fill: the drain wave of a band workgroup copies the in-group rings 1 .. wl-1 (fed by bands
+// first .. last-1) to those bands' granules, the feed of the 64-row strips below them; the I/O wave
+// still drains the last ring. A wave of its own: its write-through stores would otherwise sit in the
+// I/O wave's vmcnt in front of every granule poll (in-order completion) and slow the cross-group
+// hand-off.
 __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_int *rings, int grp, int W, int lane)
 {
     const int first = grp * W;
-    const int last = min(first + W, a.num_strips) - 1;
+    const int last = min(first + W, a.num_bands) - 1;
     const int wl = last - first + 1;
-    // dual: rings 1 .. wl-1 (fed by strips first .. last-1) go to those strips' granules as well, the
-    // direction waves' feed (the compute waves publish into LDS only)
     int dr[kMaxWaves - 1], drN[kMaxWaves - 1];
     uint64_t *drOut[kMaxWaves - 1];
     bool drPending = false;
@@ -1570,13 +1473,9 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
         dr[r] = 0;
         drN[r] = 0;
         drOut[r] = a.bnd;
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_DUAL_CSTORE)
-        if (false)
-#else
         if (r + 1 < wl)
-#endif
         {
-            const StripDesc sr = a.strips[first + r];
+            const StripDesc sr = a.bands[first + r];
             if (uniform(sr.flags) & kHasNext)
             {
                 drN[r] = (int)uniform64(a.pairs[uniform(sr.pair)].text_len);
@@ -1639,28 +1538,26 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
     const int lane = threadIdx.x & (kWave - 1);
     const int w = uniform((int)(threadIdx.x / kWave));
     // compute waves; with CHAIN wave W is the I/O wave (plans without strip chains have none, and no
-    // rings in LDS either: more workgroups fit a CU)
-    // (dual: one more wave, the drain wave W + 1)
-    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0) - (CHAIN && a.dual ? 1 : 0);
+    // rings in LDS either: more workgroups fit a CU); band launches have one more wave, the drain
+    // wave W + 1 (idle in the strip workgroups)
+    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0) - (CHAIN && a.num_bands > 0 ? 1 : 0);
     if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
-    // DUAL fill: the workgroups past the score workgroups are direction workers (no LDS, no barriers)
-    constexpr bool kDual = R == 1 && SK == kArr8 && !LOCAL && CHAIN;
-    if constexpr (kDual)
-        if (a.dual && (int)blockIdx.x >= a.score_wgs)
-        {
-#if !(defined(SA_EXPERIMENT) && defined(SA_EXP_NO_DIRWORK))
-            if (w < W) dir_worker(a, lane);  // (timing ablation: no direction work at all)
-#endif
-            return;
-        }
+    // BAND fill: workgroups [0, band_wgs) take groups of W bands from their own queue, the others
+    // groups of W strips; with one workgroup per CU (the launch's LDS request) no CU mixes the two
+    constexpr bool kBand = R == 1 && SK == kArr8 && CHAIN;
+    const bool bandRole = kBand && a.num_bands > 0 && (int)blockIdx.x < a.band_wgs;
+    const StripDesc *strips = bandRole ? a.bands : a.strips;
+    const int nstrips = bandRole ? a.num_bands : a.num_strips;
+    const int ngroups = bandRole ? a.num_band_groups : a.num_groups;
+    uint32_t *qhead = bandRole ? &a.ctrl->band_head : &a.ctrl->queue_head;
     while (true)
     {
         __syncthreads();  // every wave is done with the previous group's rings
         if (threadIdx.x == 0)
         {
             const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-            H.group = aborted ? a.num_groups : (int)atomicAdd(&a.ctrl->queue_head, 1u);
+            H.group = aborted ? ngroups : (int)atomicAdd(qhead, 1u);
             H.nwaves = W;
         }
         if (threadIdx.x <= kMaxWaves) H.cons[threadIdx.x] = H.drain[threadIdx.x] = 0;
@@ -1673,46 +1570,38 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
         }
         __syncthreads();
         const int grp = uniform(H.group);
-        if (grp >= a.num_groups) break;
+        if (grp >= ngroups) break;
         if (CHAIN && w == W)
         {
-            io_wave(a, H.cons, H.drain, rings, grp, W, lane);
+            io_wave(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane);
         }
         else if (CHAIN && w == W + 1)
         {
-            drain_wave(a, H.drain, rings, grp, W, lane);
+            if (bandRole) drain_wave(a, H.drain, rings, grp, W, lane);
         }
         else
         {
             const int idx = grp * W + w;
-            // dual: the score waves issue ahead of the I/O and drain waves sharing their SIMDs
-            // (measured -0.8 % fill, profiles/r03/dual_dev/prio_timeline.log)
-            if (CHAIN && a.dual) __builtin_amdgcn_s_setprio(2);
-            if (idx < a.num_strips)
+            if (idx < nstrips)
             {
                 // the strip kind is compile-time inside process_strip (branch-free body boundaries)
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
                 // variant is instantiated, which keeps the register count of the batch kernel down)
-                const int f = uniform(a.strips[idx].flags) & (kHasPrev | kHasNext);
-                const StripLds L{H.S, H.cons, H.nwaves, nullptr, nullptr, nullptr, H.drain};
-                if constexpr (kDual)
-                {
-                    if (a.dual)
+                const int f = uniform(strips[idx].flags) & (kHasPrev | kHasNext);
+                const StripLds L{H.S, H.cons, H.nwaves, H.drain};
+                if constexpr (kBand)
+                    if (bandRole)
                     {
-                        if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true, false, true>(a, L, rings, idx, w, lane);
-                        else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false, false, true>(a, L, rings, idx, w, lane);
-                        else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true, false, true>(a, L, rings, idx, w, lane);
-                        else process_strip<R, LOCAL, SK, false, false, false, true>(a, L, rings, idx, w, lane);
+                        // the bands issue ahead of the I/O and drain waves sharing their SIMDs (measured
+                        // -0.8 % fill for round 3's score waves, profiles/r03/dual_dev/prio_timeline.log)
+                        __builtin_amdgcn_s_setprio(2);
+                        // (every band publishes its bottom row: kHasNext)
+                        if (f & kHasPrev) process_band<LOCAL, true, true>(a, L, rings, idx, w, lane);
+                        else process_band<LOCAL, false, true>(a, L, rings, idx, w, lane);
+                        __builtin_amdgcn_s_setprio(0);
+                        continue;
                     }
-                    else
-                    {
-                        if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
-                        else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
-                        else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, L, rings, idx, w, lane);
-                        else process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
-                    }
-                }
-                else if constexpr (CHAIN)
+                if constexpr (CHAIN)
                 {
                     if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
                     else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
@@ -1748,7 +1637,7 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1 + (a.dual ? 1 : 0))), lds, st, a);
+        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1 + (a.num_bands > 0 ? 1 : 0))), lds, st, a);
     }
     else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
 }
@@ -1789,9 +1678,5 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
 }
 
 template void launch_fill_r<SA_FILL_R>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
-
-#if SA_FILL_R == 1
-#include "sa_split.inc"
-#endif
 
 }  // namespace sa

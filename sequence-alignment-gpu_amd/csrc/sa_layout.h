@@ -62,7 +62,7 @@ struct Control {
     uint32_t queue_head;   // dynamic strip queue
     uint32_t abort_flag;   // set when a hand-off times out
     uint32_t bad_input;    // set by encode_text_kernel: a text or pattern byte outside 0..A-1
-    uint32_t dir_head;     // dual fill: next direction task
+    uint32_t band_head;    // band fill: the bands' group queue
 };
 
 }  // namespace sa

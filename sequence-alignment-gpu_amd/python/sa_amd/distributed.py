@@ -48,6 +48,31 @@ def gather_array(results, num_pairs: int, world: int, rank: int, device):
     return out
 
 
+def gather_device(buf, num_pairs: int, world: int, rank: int):
+    """Gathers every rank's sa_result rows, already in a (width, 4) int64 tensor on the rank's device
+    (Plan.copy_results: bit copies of sa_result, so column 0 is score | status << 32), to rank 0 with
+    one collective and no host round trip before it; rank 0 brings the gathered block to the host in
+    one copy. Returns the (num_pairs, 4) int64 FIELDS array in global pair order on rank 0, None
+    elsewhere (as gather_array)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0)
+    if rank != 0:
+        return None
+    allp = torch.stack(parts).cpu().numpy()
+    out = np.empty((num_pairs, len(FIELDS)), np.int64)
+    for r in range(world):
+        idx = shard(num_pairs, world, r)
+        rows = allp[r, : len(idx)]
+        score = rows[:, 0] & 0xFFFFFFFF
+        out[idx, 0] = np.where(score >= 1 << 31, score - (1 << 32), score)
+        out[idx, 1:] = rows[:, 1:]
+    return out
+
+
 def gather_results(results, num_pairs: int, world: int, rank: int, device) -> list[dict] | None:
     """Gathers every rank's per-pair results to rank 0 in global pair order; None on other ranks."""
     import torch

@@ -19,7 +19,7 @@ STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4
 
 # Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
-           "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results",
+           "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results", "sa_plan_copy_results",
            "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace",
            "sa_plan_output_bytes", "sa_plan_fetch_all", "sa_align_batch", "sa_batch_deal", "sa_build_id",
            "sa_batch_last_stats")
@@ -72,6 +72,8 @@ def _load():
     L.sa_plan_fetch_directions.argtypes = [P, ctypes.c_int64, P, P]
     L.sa_plan_device_results.argtypes = [P]
     L.sa_plan_device_results.restype = P
+    L.sa_plan_copy_results.argtypes = [P, P, P]
+    L.sa_plan_copy_results.restype = I
     L.sa_device_count.argtypes = [ctypes.POINTER(I)]
     L.sa_last_error.restype = ctypes.c_char_p
     L.sa_selftest.argtypes = [I]
@@ -244,6 +246,10 @@ class Plan:
         out = np.empty(max(1, self.num_pairs), RESULT_DTYPE)
         _check(lib.sa_plan_fetch_results(self.handle, out.ctypes.data, stream))
         return out[: self.num_pairs]
+
+    def copy_results(self, d_dst: int, stream: int | None = None) -> None:
+        """Asynchronous device-to-device copy of every pair's sa_result (32 bytes each) to d_dst."""
+        _check(lib.sa_plan_copy_results(self.handle, d_dst, stream))
 
     def directions(self, index: int, stream: int | None = None) -> np.ndarray:
         """Decoded (m+1)x(n+1) DIRECTION matrix of pair `index` (reference layout, for verification)."""

@@ -124,3 +124,75 @@ def test_gather_array_world2():
         st = -1 if i % 3 == 0 else i  # (uint64)-1 as its int64 bit pattern
         assert got[i].tolist() == [10 * i - 7, i + 3, st, i * 5], i
     assert np.uint64(got[0, 2].view(np.uint64)) == np.uint64((1 << 64) - 1)
+
+
+def _device_worker(rank, world, port, num, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from sa_amd import distributed
+    from sa_amd.engine import RESULT_DTYPE
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = distributed.shard(num, world, rank)
+    arr = np.zeros(len(mine), RESULT_DTYPE)
+    arr["score"] = [10 * i - 7 for i in mine]
+    arr["status"] = [i % 2 for i in mine]  # the word beside the score must not leak into it
+    arr["num_bytes"] = [i + 3 for i in mine]
+    arr["start_text"] = [(1 << 64) - 1 if i % 3 == 0 else i for i in mine]
+    arr["start_pattern"] = [i * 5 for i in mine]
+    # what Plan.copy_results leaves in the bench's gather buffer: raw sa_result bytes, (width, 4) int64
+    buf = torch.full(((num + world - 1) // world, 4), -1, dtype=torch.int64)
+    buf[: len(mine)] = torch.from_numpy(arr.view(np.int64).reshape(len(mine), 4).copy())
+    out = distributed.gather_device(buf, num, world, rank)
+    if rank == 0:
+        q.put(out)
+    dist.destroy_process_group()
+
+
+def test_gather_device_world2():
+    """The bench's device-resident result path: raw sa_result rows (Plan.copy_results) -> rank 0 in
+    one gather; score is the low int32 of the first word, uint64 starts keep their bits."""
+    num = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_device_worker, args=(r, 2, port, num, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got.shape == (num, 4)
+    for i in range(num):
+        st = -1 if i % 3 == 0 else i
+        assert got[i].tolist() == [10 * i - 7, i + 3, st, i * 5], i
+
+
+def test_bench_launches_ranks_dry_run():
+    """`bench.py --gpus 2` without WORLD_SIZE starts its own two ranks (torch.distributed.run) and the
+    rank-0 line reports n_gpus 2 (--dry-run: gloo, no GPU work)."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                          "--dry-run"], env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    assert lines[0]["n_gpus"] == 2 and lines[0]["ranks_seen"] == 2 and lines[0]["steps"] == 3
+
+
+def test_bench_refuses_world_size_mismatch():
+    """WORLD_SIZE (set by a launcher) must equal --gpus: a silent one-GPU line for --gpus 8 is refused."""
+    import subprocess
+    import sys
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"], env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode != 0 and "WORLD_SIZE" in out.stderr

@@ -52,12 +52,13 @@ OUT = os.environ.get("SA_GEN_FILL_OUT") or os.path.join(ROOT, "sequence-alignmen
 U = 16
 # with a strip above, the next body's feed read is issued after this step (kPfLead = U - PF_STEP)
 PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "14"))
-# the dual fill's score steps (rec_steps_asm) are shorter, so their read takes more steps of lead:
-# after step 10 measured 1 % faster than after 14 (profiles/r03/dual_dev/pf_timeline.log)
-REC_PF_STEP = int(os.environ.get("SA_GEN_REC_PF_STEP", "10"))
+# the band fill's score steps (band_steps_asm) read the next feed after this step (kPfLead = U - it);
+# a 44-clock step leaves two steps too little time for the LDS read (the R = 1 score steps of round 3
+# measured 1 % faster after step 10 than after 14, profiles/r03/dual_dev/pf_timeline.log)
+BAND_PF_STEP = int(os.environ.get("SA_GEN_BAND_PF_STEP", "10"))
 
 
-def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) -> str:
+def block(local: bool, hn: bool, hp: bool, half: int) -> str:
     # named operands (the C++ wrapper below binds them)
     A, B, C, FA = "%[q]", "%[qn]", "%[dg]", "%[f]"
     D, M, T0 = "%[d]", "%[m]", "%[t0]"
@@ -81,19 +82,12 @@ def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) ->
         g, byte = 4 * half + (q & 3), 3 - (q >> 2)
         sd = f"dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
-        if hp and q == (REC_PF_STEP if rec_only else PF_STEP):
+        if hp and q == PF_STEP:
             out.append(f"ds_read_b32 {PF}, {PFA}")
         if hn:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf")
         else:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-        if rec_only:
-            # b, d, c, max3: c (DPP of F) stands two instructions behind the max3 that wrote F
-            out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
-                       f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
-            out.append(f"v_mov_b32_dpp {qr}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
-            out.append(f"v_max3_i32 {dg}, {D}, {fp}, {qr}")
-            continue
         out.append(f"v_mov_b32_dpp {qr}, {fp} wave_shr:1 row_mask:0xf bank_mask:0xf")
         out.append(f"v_add_u32_sdwa {D}, {dg}, sext({TW[q >> 2]}) dst_sel:DWORD dst_unused:UNUSED_PAD "
                    f"src0_sel:DWORD src1_sel:BYTE_{q & 3}")
@@ -131,6 +125,73 @@ def block(local: bool, hn: bool, hp: bool, half: int, rec_only: bool = False) ->
     return "\\n\\t".join(out)
 
 
+def band_block(local: bool, hn: bool, hp: bool) -> str:
+    """U = 16 steps of a band score strip: two rows per lane (rows 2k, 2k+1 of a 128-row band), the
+    recurrence alone (no direction bits). Eight registers P0..P7 rotate with period 8: at step k the
+    register of phase p is P[(k - p) % 8], and the phases are
+        p = 0  F1 of step k-2 (dead): the queue shift Qn is written here (lane 63 keeps F1, HN)
+        p = 1  Q (the feed queue); up = wave_shr:1(F1 of step k-1) in place (lane 0 keeps the feed)
+        p = 2  up of step k-1 (= diag of row 0): D0 = diag0 + S0 in place, then F0 = max3(D0, F0', up)
+        p = 3  F0 of step k-1 (left of row 0, diag of row 1)
+        p = 6  D1 = F0 of step k-1 + S1, then F1 = max3(D1, F1', F0)
+        p = 7  F1 of step k-1 (left of row 1; the DPP's source)
+        p = 4, 5  free
+    (local: H = X - g saturated at 0, one v_sub_u32 with clamp after each max3; X >= 0). The up-DPP
+    stands three instructions behind the max3 (and the subtract) that wrote F1, the queue shift two;
+    a body of 16 steps returns every value to its register. 6 VALU per step (8 local)."""
+    P = [f"%[p{i}]" for i in range(8)]
+    T0 = [f"%[ta{i}]" for i in range(4)]
+    T1 = [f"%[tb{i}]" for i in range(4)]
+    G, T = "%[g]", "%[t0]"
+    PF, BAD, PFA, CTAG, PADDR, PTAG, MSB = "%[pf]", "%[bad]", "%[pfa]", "%[ctag]", "%[paddr]", "%[ptag]", "%[msb]"
+    out = ["s_nop 1"]  # the compiler's last writes of Q / F1 may stand right before
+    for k in range(U):
+        ph = lambda p: P[(k - p) % 8]
+        sel = f"dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_{k & 3}"
+        out.append(f"v_add_u32_sdwa {ph(2)}, {ph(2)}, sext({T0[k >> 2]}) {sel}")
+        out.append(f"v_add_u32_sdwa {ph(6)}, {ph(3)}, sext({T1[k >> 2]}) {sel}")
+        if hp and k == BAND_PF_STEP:
+            out.append(f"ds_read_b32 {PF}, {PFA}")
+        bc = "" if hn else " bound_ctrl:1"
+        out.append(f"v_mov_b32_dpp {ph(0)}, {ph(1)} wave_shl:1 row_mask:0xf bank_mask:0xf{bc}")
+        out.append(f"v_mov_b32_dpp {ph(1)}, {ph(7)} wave_shr:1 row_mask:0xf bank_mask:0xf")
+        out.append(f"v_max3_i32 {ph(2)}, {ph(2)}, {ph(3)}, {ph(1)}")
+        if local:
+            out.append(f"v_sub_u32_e64 {ph(2)}, {ph(2)}, {G} clamp")
+        out.append(f"v_max3_i32 {ph(6)}, {ph(6)}, {ph(7)}, {ph(2)}")
+        if local:
+            out.append(f"v_sub_u32_e64 {ph(6)}, {ph(6)}, {G} clamp")
+    if hp:
+        out.append("s_waitcnt lgkmcnt(0)")
+        out.append(f"v_bitop3_b32 {PF}, {PF}, {CTAG}, {MSB} bitop3:0xd2")
+        out.append(f"v_cmp_gt_i32_e64 {BAD}, 0, {PF}")
+        out.append(f"s_and_b64 {BAD}, {BAD}, 0xffff")
+    if hn:
+        # k = 16: phase 0 = P0 holds F1 of step 14, phase 1 = P7 the queue: one more shift gives lanes
+        # 48..63 = F1 of steps s0-1 .. s0+14 (as the one-wave bodies publish)
+        out.append(f"v_mov_b32_dpp {P[0]}, {P[7]} wave_shl:1 row_mask:0xf bank_mask:0xf")
+        out.append(f"v_bitop3_b32 {T}, {P[0]}, {PTAG}, {MSB} bitop3:0xf2")
+        out.append(f"ds_write_b32 {PADDR}, {T}")
+    return "\\n\\t".join(out)
+
+
+def band_operands(local: bool, hn: bool, hp: bool):
+    # at entry / exit: Q = P7 (phase 1), diag0 = P6 (phase 2), F0 = P5 (phase 3), F1 = P1 (phase 7)
+    outs = ['[p7] "+v"(r.Q)', '[p6] "+v"(r.diag)', '[p5] "+v"(r.F0)', '[p1] "+v"(r.F1)',
+            '[p0] "=&v"(x0)', '[p2] "=&v"(x2)', '[p3] "=&v"(x3)', '[p4] "=&v"(x4)', '[t0] "=&v"(t0)']
+    ins = [f'[ta{i}] "v"(r.TA[{i}])' for i in range(4)] + [f'[tb{i}] "v"(r.TB[{i}])' for i in range(4)]
+    if local:
+        ins += ['[g] "s"(r.g)']
+    if hp:
+        outs += ['[pf] "=&v"(r.pf)', '[bad] "=&s"(r.bad)']
+        ins += ['[pfa] "v"(r.pfaddr)', '[ctag] "s"(r.ctag)']
+    if hn:
+        ins += ['[paddr] "v"(r.pubaddr)', '[ptag] "s"(r.pubtag)']
+    if hn or hp:
+        ins += ['[msb] "v"(r.msb)']
+    return outs, ins
+
+
 def merge(local: bool) -> str:
     """The chunk's sign bits into its two interleaved words a0 (slots 0..15), a1 (slots 16..31)."""
     out = []
@@ -165,11 +226,10 @@ def merge(local: bool) -> str:
     return "\\n\\t".join(out)
 
 
-def operands(local: bool, hn: bool, hp: bool, rec_only: bool = False):
+def operands(local: bool, hn: bool, hp: bool):
     outs = ['[q] "+v"(r.Q)', '[qn] "=&v"(r.Qn)', '[dg] "+v"(r.diag)', '[f] "+v"(r.F)',
             '[d] "=&v"(D)', '[m] "=&v"(M)', '[t0] "=&v"(t0)']
-    if not rec_only:
-        outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
+    outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
     ins = [f'[tw{i}] "v"(r.T[{i}])' for i in range(4)]
     if local:
         outs += [f'[z{g}] "+v"(r.Z[{g}])' for g in range(8)]
@@ -195,26 +255,26 @@ def main():
         "// of its chunk); Q / Qn / diag / F rotate through the roles with period 4 (back in place after",
         "// the body); with HP the next body's feed read (address r.pfaddr) is issued after step 12 and",
         "// waited for at the end (result r.pf). merge_asm<LOCAL>(r) builds the chunk's two words.",
-        "// rec_steps_asm<HN, HP>(r): the dual fill's score-wave steps (global, no direction bits).",
+        "// band_steps_asm<LOCAL, HN, HP>(r): the band fill's score-wave steps (two rows per lane, no",
+        "// direction bits; see band_block in the generator).",
         "#pragma once",
         "",
     ]
-    # the dual fill's score waves (global): the recurrence alone, F = max3(D, left, up), 4 VALU per
-    # step (b, d, c, max3: the up-DPP c stands two instructions behind the max3 that wrote F)
-    for hn in (False, True):
-        for hp in (False, True):
-            body = block(False, hn, hp, 0, rec_only=True)
-            outs, ins = operands(False, hn, hp, rec_only=True)
-            lines.append(f"template <> __device__ __forceinline__ void rec_steps_asm<{str(hn).lower()}, "
-                         f"{str(hp).lower()}>(StepRegs &r)")
-            lines.append("{")
-            lines.append("    int D, M, t0;")
-            lines.append(f"    asm volatile(\"{body}\"")
-            lines.append("        : " + ", ".join(outs))
-            lines.append("        : " + ", ".join(ins) + (" : \"scc\");" if hp else ");"))
-            lines.append("    (void)D; (void)M; (void)t0;")
-            lines.append("}")
-            lines.append("")
+    for local in (False, True):
+        for hn in (False, True):
+            for hp in (False, True):
+                body = band_block(local, hn, hp)
+                outs, ins = band_operands(local, hn, hp)
+                lines.append(f"template <> __device__ __forceinline__ void band_steps_asm<{str(local).lower()}, "
+                             f"{str(hn).lower()}, {str(hp).lower()}>(BandRegs &r)")
+                lines.append("{")
+                lines.append("    int x0, x2, x3, x4, t0;")
+                lines.append(f"    asm volatile(\"{body}\"")
+                lines.append("        : " + ", ".join(outs))
+                lines.append("        : " + ", ".join(ins) + (" : \"scc\");" if hp else ");"))
+                lines.append("    (void)x0; (void)x2; (void)x3; (void)x4; (void)t0;")
+                lines.append("}")
+                lines.append("")
     for local in (False, True):
         for hn in (False, True):
             for hp in (False, True):
