@@ -7,3 +7,4 @@ for w in headline local dna8k protein4k; do
   timeout -k 10 200 python bench.py --workload $w --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/b1_$w.json 2> gpurun_out/b1_$w.err || { tail -n 20 gpurun_out/b1_$w.err; exit 1; }
   python tools/show_bench.py gpurun_out/b1_$w.json
 done
+bash tools/timeline.sh -m "32768" -o "0 1" -f "total_us ns_per_step_mean lag_ns_in_group_mean lag_ns_cross_group_mean last_start_us bands"

@@ -29,6 +29,47 @@ def max_overlap(xcc, se, cu, simd, fed, end):
     return best
 
 
+def summarize(tl, n, W, t0=None):
+    """Chain statistics of consecutive records (strips, or bands) of one pair."""
+    start, fed, end = (tl[:, i].astype(np.int64) for i in range(3))
+    xcc = (tl[:, 3] >> 32).astype(np.int64)
+    hw = (tl[:, 3] & 0xffffffff).astype(np.int64)
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    t0 = start.min() if t0 is None else t0
+    nsteps = n + 63
+    lag = np.diff(fed) * 10.0 if len(fed) > 1 else np.zeros(1)  # ns
+    step_ns = (end - fed) * 10.0 / nsteps
+    clk = (tl[:, 5].astype(np.int64) - tl[:, 4].astype(np.int64))
+    mhz = clk / np.maximum(1, (end - fed)) * 100.0  # s_memtime ticks per s_memrealtime (100 MHz) tick
+    k = np.arange(1, len(fed))
+    cross = (k % W) == 0
+    return {
+        "records": len(fed),
+        "total_us": round((end.max() - t0) * 0.01, 2),
+        "first_fed_us": round((fed[0] - t0) * 0.01, 3),
+        "last_start_us": round((start[-1] - t0) * 0.01, 2),
+        "last_end_us": round((end[-1] - t0) * 0.01, 2),
+        "ns_per_step_mean": round(float(step_ns.mean()), 2),
+        "ns_per_step_min": round(float(step_ns.min()), 2),
+        "ns_per_step_max": round(float(step_ns.max()), 2),
+        "lag_ns_in_group_mean": round(float(lag[~cross].mean()), 1) if (~cross).any() else None,
+        "lag_ns_cross_group_mean": round(float(lag[cross].mean()), 1) if cross.any() else None,
+        "lag_ns_p50": round(float(np.percentile(lag, 50)), 1),
+        "lag_ns_p90": round(float(np.percentile(lag, 90)), 1),
+        "lag_ns_max": round(float(lag.max()), 1),
+        "start_wait_ns_mean": round(float(((fed - start) * 10.0).mean()), 1),
+        "shader_mhz_mean": round(float(mhz.mean()), 1),
+        "clk_per_step_mean": round(float((clk / nsteps).mean()), 1),
+        "ns_per_step_by_strip": [round(float(x), 1) for x in step_ns[:: max(1, len(step_ns) // 16)]],
+        "lag_ns_by_strip": [round(float(x), 1) for x in lag[:: max(1, len(lag) // 16)]],
+        "fed_us_by_strip": [round(float((x - t0) * 0.01), 2) for x in fed[:: max(1, len(fed) // 16)]],
+        "cus_used": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
+        "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
+        "ns_per_step_by_wave_in_group": [round(float(step_ns[w::W].mean()), 2) for w in range(W)],
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=32768)
@@ -62,66 +103,17 @@ def main():
     tl = np.fromfile(path, dtype=np.uint64).reshape(-1, 48)
     if os.environ.get("SA_TL_SAVE"):
         np.save(os.environ["SA_TL_SAVE"], tl)  # raw records for offline analysis
-    start, fed, end = (tl[:, i].astype(np.int64) for i in range(3))
-    xcc = (tl[:, 3] >> 32).astype(np.int64)
-    hw = (tl[:, 3] & 0xffffffff).astype(np.int64)
-    cu = (hw >> 8) & 0xF
-    se = (hw >> 13) & 0x7
-    t0 = start.min()
-    nsteps = args.n + 63
-    lag = np.diff(fed) * 10.0 if len(fed) > 1 else np.zeros(1)  # ns
-    step_ns = (end - fed) * 10.0 / nsteps
-    clk = (tl[:, 5].astype(np.int64) - tl[:, 4].astype(np.int64))
-    mhz = clk / np.maximum(1, (end - fed)) * 100.0  # s_memtime ticks per s_memrealtime (100 MHz) tick
     W = int(os.environ.get("SA_WAVES_PER_GROUP", "4"))
-    # the split fill (R = 1 global int8-profile chains) runs SA_SPLIT_W strips per workgroup
-    split = args.mode == 0 and args.R == 1 and args.m > 64 and os.environ.get("SA_SPLIT", "0") != "0"
-    if split:
-        W = int(os.environ.get("SA_SPLIT_W", "2"))
-    k = np.arange(1, len(fed))
-    cross = (k % W) == 0
-    rec = {
-        "n": args.n, "m": args.m, "R": args.R, "W": W, "pairs": args.pairs, "strips": len(fed),
-        "total_us": round((end.max() - t0) * 0.01, 2),
-        "first_fed_us": round((fed[0] - t0) * 0.01, 3),
-        "last_start_us": round((start[-1] - t0) * 0.01, 2),
-        "ns_per_step_mean": round(float(step_ns.mean()), 2),
-        "ns_per_step_min": round(float(step_ns.min()), 2),
-        "ns_per_step_max": round(float(step_ns.max()), 2),
-        "lag_ns_in_group_mean": round(float(lag[~cross].mean()), 1) if (~cross).any() else None,
-        "lag_ns_cross_group_mean": round(float(lag[cross].mean()), 1) if cross.any() else None,
-        "lag_ns_p50": round(float(np.percentile(lag, 50)), 1),
-        "lag_ns_p90": round(float(np.percentile(lag, 90)), 1),
-        "lag_ns_max": round(float(lag.max()), 1),
-        "start_wait_ns_mean": round(float(((fed - start) * 10.0).mean()), 1),
-        "shader_mhz_mean": round(float(mhz.mean()), 1),
-        "shader_mhz_min": round(float(mhz.min()), 1),
-        "clk_per_step_mean": round(float((clk / nsteps).mean()), 1),
-        "ns_per_step_by_strip": [round(float(x), 1) for x in step_ns[:: max(1, len(step_ns) // 16)]],
-        "lag_ns_by_strip": [round(float(x), 1) for x in lag[:: max(1, len(lag) // 16)]],
-        "xcc_of_first_16": xcc[:16].tolist(),
-        "cu_se_of_first_8": [(int(c), int(s)) for c, s in zip(cu[:8], se[:8])],
-        "cus_used": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
-        "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
-        "simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in hw[:8]],
-        # pace by the strip's wave slot in its group and by its SIMD (does the wave that shares its
-        # SIMD with the group's I/O wave run slower?)
-        "ns_per_step_by_wave_in_group": [round(float(step_ns[w::W].mean()), 2) for w in range(W)],
-        "ns_per_step_by_simd": [round(float(step_ns[((hw >> 4) & 3) == q].mean()), 2) if (((hw >> 4) & 3) == q).any() else None for q in range(4)],
-    }
-    if split:
-        # dir waves (timeline words 42..46): how far each ends behind its score wave, how often it
-        # found its body unfinished, how often the score wave waited for it, and where it ran
-        dend = tl[:, 43].astype(np.int64)
-        dhw = (tl[:, 46] & 0xffffffff).astype(np.int64)
-        rec["split"] = {
-            "dir_end_behind_score_ns_mean": round(float(((dend - end) * 10.0).mean()), 1),
-            "dir_waiting_polls_mean": round(float(tl[:, 44].astype(np.int64).mean()), 1),
-            "score_waits_for_dir_mean": round(float(tl[:, 45].astype(np.int64).mean()), 2),
-            "dir_simd_wave_of_first_8": [(int((h >> 4) & 3), int(h & 15)) for h in dhw[:8]],
-        }
-    prog = tl[:, 6:16].astype(np.int64)
-    iop = tl[:, 16:26].astype(np.int64)
+    ns = args.pairs * ((args.m + 64 * args.R - 1) // (64 * args.R))
+    t0 = int(tl[:, 0].astype(np.int64).min())
+    rec = {"n": args.n, "m": args.m, "R": args.R, "W": W, "pairs": args.pairs, "strips": ns}
+    rec.update(summarize(tl[:ns], args.n, W, t0))
+    if len(tl) > ns:
+        # band fill: the band records follow the strips' (one pair's chain)
+        nb = (len(tl) - ns) // args.pairs
+        rec["bands"] = summarize(tl[ns:ns + nb], args.n, W, t0)
+    prog = tl[:ns, 6:16].astype(np.int64)
+    iop = tl[:ns, 16:26].astype(np.int64)
     if prog[:, 1].any():
         # experiment builds (SA_EXP_PROGRESS): time at columns 0, 4096, ... per strip; the lag between
         # consecutive strips at each checkpoint shows whether a consumer falls behind its producer
@@ -143,13 +135,13 @@ def main():
         # reached column 4096q (negative: the feed was there first, the strip was the bottleneck)
         gi = [k for k in range(W, len(prog), W) if iop[k, 1] > 0]
         rec["io_ahead_us_every8groups"] = [[k] + [round(float(prog[k, q] - iop[k, q]) * 0.01, 1) for q in range(1, 9) if iop[k, q] > 0 and prog[k, q] > 0] for k in gi[::8]]
-        mt = tl[:, 26:36].astype(np.int64)
+        mt = tl[:ns, 26:36].astype(np.int64)
         segc = np.diff(mt[:, ok], axis=1) / 4096.0
         rec["clk_per_step_by_segment_every32"] = [[k] + [round(float(x), 1) for x in segc[k]] for k in range(0, len(segc), 32)]
         rec["checkpoint_us"] = [[k] + [round(float(x - t0) * 0.01, 1) for x in prog[k, ok]] for k in range(0, len(seg), 64)]
         # slow-path counters per strip: feed checks that failed / their re-reads, publishes that
         # waited for the consumer / their polls (bodies per strip = nsteps / 16)
-        sc = tl[:, 36:42].astype(np.int64)
+        sc = tl[:ns, 36:42].astype(np.int64)
         rec["slow_paths_mean_per_strip"] = {nm: round(float(sc[1:, i].mean()), 1) for i, nm in
                                             enumerate(("feed_slow", "feed_spins", "pub_slow", "pub_spins",
                                                        "feed_slow_past_4096", "feed_spins_past_4096"))}
