@@ -196,6 +196,8 @@ struct Knobs {
                                     // default: on wherever it applies (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
+    int io_probe = 1;               // SA_IO_PROBE: 0 = full-window polls while a group waits for its
+                                    // first column too
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
     const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
@@ -214,6 +216,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_BAND")) v.band = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
         if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
+        if (const char *e = get("SA_IO_PROBE")) v.io_probe = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
         v.timeline = get("SA_TIMELINE");
         v.tb_timing = get("SA_TB_TIMING");
@@ -968,6 +971,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.key_rowbits = pl->key_rowbits;
         a.timeout_ticks = (uint64_t)(knobs().handoff_timeout_s * 1e8);
         a.io_sleep = knobs().io_sleep;
+        a.io_probe = knobs().io_probe;
         a.chain_lds = knobs().chain_lds_kb * 1024;
         a.bands = pl->d_bands;
         a.num_bands = 0;

@@ -88,7 +88,7 @@ constexpr int kRingMask = kRing - 1;
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_DIRWORK)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -1380,13 +1380,24 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
             want = min(min(kIoWin * kWave, nIn - copied), room);
             if (want < min(16, nIn - copied)) want = 0;
         }
-        // every poll loads whole windows (one round trip from the producer's store to the ring; a
-        // lane-0 probe first would add a second): a few KiB per poll per waiting group is nothing
-        // next to the fill's own traffic
+        // polls load whole windows (one round trip from the producer's store to the ring; a lane-0
+        // probe first would add a second), except while the group waits for its first column (up to
+        // hundreds of microseconds for the late groups of a band launch, all polling at once): then
+        // lane 0 probes that column's 8 bytes, and the first full poll follows its match
+        const bool probe = a.io_probe && copied == 0;
         sfor<kIoWin>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
-            v[q] = q * kWave + lane < want ? load_granule(bin + copied + q * kWave + lane) : 0;
+            v[q] = q * kWave + lane < (probe ? 1 : want) ? load_granule(bin + copied + q * kWave + lane) : 0;
         });
+        if (probe && want > 0 && uniform((int)((uint32_t)(v[0] >> 32) == a.epoch)) == 0)
+            want = -1;  // nothing yet: no copy this round (the drain below still runs)
+        else if (probe && want > 0)
+        {
+            sfor<kIoWin>([&](auto Qc) {
+                constexpr int q = decltype(Qc)::value;
+                v[q] = q * kWave + lane < want ? load_granule(bin + copied + q * kWave + lane) : 0;
+            });
+        }
         // 2. drain ring[W'] into granules for the next group (up to kIoWin windows)
         for (int rep = 0; rep < kIoWin && drained < nOut; ++rep)
         {
@@ -1409,6 +1420,7 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
         // 3. the poll's result -> ring[0]
         int total = 0;  // ready prefix over the windows
         bool open = want > 0;
+        if (want < 0) want = 0;
         sfor<kIoWin>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
             if (!open) return;
@@ -1551,6 +1563,9 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
     const int nstrips = bandRole ? a.num_bands : a.num_strips;
     const int ngroups = bandRole ? a.num_band_groups : a.num_groups;
     uint32_t *qhead = bandRole ? &a.ctrl->band_head : &a.ctrl->queue_head;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STRIPS)
+    if (kBand && a.num_bands > 0 && !bandRole) return;  // timing ablation: the bands alone (results wrong)
+#endif
     while (true)
     {
         __syncthreads();  // every wave is done with the previous group's rings
