@@ -88,7 +88,7 @@ constexpr int kRingMask = kRing - 1;
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -947,6 +947,9 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     const __amdgpu_buffer_rsrc_t crsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
     auto load_codes = [&](int s0, int (&dA)[4], int (&dB)[4]) __attribute__((always_inline)) {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_CODES_CONST)
+        s0 &= 63;  // timing ablation: cache-resident text codes (results wrong)
+#endif
         const i32x4u va = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[0], s0, 0);
         const i32x4u vb = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[1], s0, 0);
         dA[0] = va.x;
@@ -1592,7 +1595,13 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
         }
         else if (CHAIN && w == W + 1)
         {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_DRAIN)
+            // timing ablation: no copies of the in-group rings to granules (the strips starve)
+            if (bandRole && lane == 0)
+                for (int r = 1; r <= W; ++r) lds_st((lds_int *)&H.drain[r], 1 << 30);
+#else
             if (bandRole) drain_wave(a, H.drain, rings, grp, W, lane);
+#endif
         }
         else
         {

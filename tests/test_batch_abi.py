@@ -81,3 +81,25 @@ def test_cpp_batch_api_vs_cpu(eng):
         assert out.returncode == 0, out.stdout + out.stderr
         res = json.loads(out.stdout.strip().splitlines()[-1])
         assert res["mismatches"] == 0 and res["requests"] == int(args[1]), res
+
+
+@pytest.mark.gpu
+def test_align_batch_repeated_calls_reuse_and_rebuild(eng):
+    """sa_align_batch keeps each shard's arenas and plan across calls: the same shapes with new
+    letters (plan reused: the results must follow the new inputs), then other shapes and another
+    gap (plans rebuilt), then the first batch again, each against the oracle."""
+    import oracle
+    S = synthetic.blast_matrix()
+
+    def batch(seed, n, m, k):
+        ts = [synthetic.random_sequence(seed + 2 * i, n + 3 * i, 4) for i in range(k)]
+        ps = [synthetic.mutate(t, seed + 2 * i + 1, 4, m + i) for i, t in enumerate(ts)]
+        return ts, ps
+
+    calls = [(batch(500, 400, 380, 6), 5), (batch(600, 400, 380, 6), 5), (batch(700, 900, 700, 5), 3),
+             (batch(500, 400, 380, 6), 5)]
+    for (ts, ps), gap in calls:
+        for mode in (0, 1):
+            got = engine.align_batch(mode, ts, ps, S, gap, num_gpus=2)
+            for k in range(len(ts)):
+                assert got[k] == oracle.align(mode, ts[k], ps[k], S, gap), (mode, gap, k)
