@@ -202,6 +202,7 @@ struct Knobs {
     const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
+    bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
 };
 
 const Knobs &knobs()
@@ -221,6 +222,7 @@ const Knobs &knobs()
         v.timeline = get("SA_TIMELINE");
         v.tb_timing = get("SA_TB_TIMING");
         v.tb_generic = get("SA_TB_GENERIC") != nullptr;
+        if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
         return v;
     }();
     return k;
@@ -1061,6 +1063,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     w.gap = pl->gap;
     w.key_rowbits = pl->key_rowbits;
     w.fast = kn.tb_generic ? 0 : 1;
+    w.stager = kn.tb_stager ? 1 : 0;
     launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "walk kernel")) return rc;

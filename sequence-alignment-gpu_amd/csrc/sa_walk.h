@@ -42,6 +42,7 @@ struct WalkArgs {
     uint64_t *timing;            // debug (SA_TB_TIMING): per pair {walk start, walk end}
     int32_t gap, key_rowbits;
     int32_t fast;                // 1: unrolled asm strip walk (0: the generic loop only; tests)
+    int32_t stager;              // 1: row walk with the stager wave (0: the walker stages every strip)
 };
 
 struct ExpandArgs {

@@ -139,6 +139,42 @@ __device__ __forceinline__ void rw_stage(const uint32_t *__restrict__ sb, const 
     }
 }
 
+// Row walk, stager wave: kStageWin windows of the calling lane's row for origin column jo (window w,
+// bit pair c = column jo - 16w - c, as rw_stage), from the strip's planes in global memory, into
+// dst[w * 64 + lane] (LDS). The walker takes any eight consecutive of them.
+constexpr int kStageWin = 24;  // 384 columns: the walker's entry may lie up to 256 columns below the origin
+template <bool LOCAL>
+__device__ __forceinline__ void rw_stage_far(const uint32_t *__restrict__ sb, int jo, int lane, uint32_t *dst)
+{
+    const int etop = jo - 1 + lane;
+    const int c0 = etop >> 5;
+    const bool hi = (etop & 16) != 0;
+    const int sh = 30 - 2 * (etop & 15);
+    constexpr int NP = (kStageWin + 3) / 2;  // chunk pairs: dwords 2c0+1 .. 2c0 - 2 NP + 2
+    uint32_t L[2 * NP];
+    sfor<NP>([&](auto Qc) {
+        constexpr int q = decltype(Qc)::value;
+        const int c = c0 - q;
+        const u32x2 v = *reinterpret_cast<const u32x2 *>(sb + (int64_t)max(c, 0) * kChunkDw + lane * 2);
+        L[2 * q] = c >= 0 ? v.y : 0u;
+        L[2 * q + 1] = c >= 0 ? v.x : 0u;
+    });
+    sfor<kStageWin>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        const uint32_t lo = hi ? L[w] : L[w + 1], up = hi ? L[w + 1] : L[w + 2];
+        uint32_t x = __builtin_amdgcn_alignbit(up, lo, sh);
+        if constexpr (!LOCAL) x &= ~((x >> 1) & 0x55555555u);
+        const int z = jo - 16 * w;  // pair of column 0 (uniform): columns < 1 cleared, column 0 the border
+        if (z < 16)
+        {
+            const uint32_t vm = z <= 0 ? 0u : ((1u << (2 * z)) - 1u);
+            const uint32_t c0b = (z >= 0) ? (LOCAL ? 3u : 1u) << (2 * z) : 0u;
+            x = (x & vm) | c0b;
+        }
+        dst[w * kWave + lane] = x;
+    });
+}
+
 // Column walk: the eight windows of the calling lane's column j = J0 - 63 + lane for the row blocks
 // G0, G0-1, ..., G0-7 (block G = pair rows 16G+1 .. 16G+16; bit pair c = row 16G + 16 - c). Block -1
 // is the row-0 border. mb = the pair's first strip's first dword.
@@ -431,13 +467,59 @@ __device__ __forceinline__ bool walk_start(const WalkArgs &a, int p, int n, int 
     return false;
 }
 
-// Row walk (R = 1): one wave per pair
+// Row walk (R = 1): a walker wave and a stager wave per pair. The walker runs the rows' scalar chain;
+// at the start of strip b it asks the stager for strip b-1's windows with origin = strip b's entry
+// column (the path only moves left, so strip b-1's entry lies at or left of it), and the stager builds
+// kStageWin of them (384 columns) into LDS while the walker walks strip b. When the walker reaches
+// strip b-1 and the stager is done and covers the entry column, eight LDS reads replace the staging
+// (≈ 20 of the ≈ 85 clocks per row were staging); otherwise the walker stages as before.
+// Request words (LDS): [0] sequence number of the last request (-1: quit), [1] strip, [2] origin,
+// [3] the last sequence number the stager finished. One wave's LDS operations execute in order, so
+// the fields written before [0] / the windows written before [3] are there when it is seen.
 template <bool LOCAL>
-__global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
+__device__ void rw_stager(const WalkArgs &a, const uint32_t *mb, int64_t sstride, volatile int *req, uint32_t (*swin)[kStageWin * kWave],
+                          int lane)
+{
+    int seen = 0;
+    for (uint32_t spin = 1;; ++spin)
+    {
+        const int q = uniform(req[0]);
+        if (q < 0) return;
+        if (q == seen)
+        {
+            if (spin > 64) __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        seen = q;
+        spin = 0;
+        const int b = uniform(req[1]), O = uniform(req[2]);
+        rw_stage_far<LOCAL>(mb + (int64_t)b * sstride, O, lane, swin[q & 1]);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the windows before the done word)
+        if (lane == 0) req[3] = q;
+    }
+}
+
+template <bool LOCAL>
+__global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
 {
     __shared__ uint32_t pfbuf[2][kPfDw];
+    __shared__ uint32_t swin[2][kStageWin * kWave];
+    __shared__ int req[4];
     const int p = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & (kWave - 1);
+    if (threadIdx.x < 4) req[threadIdx.x] = 0;
+    __syncthreads();
+    if (threadIdx.x >= kWave)
+    {
+        // the stager: strips of the pair's chain (R = 1 layout, as the walker computes below)
+        const PairDesc sp = a.pairs[p];
+        if (uniform(sp.num_strips) > 0 && uniform((int)sp.text_len) > 0)
+        {
+            const StripDesc s0 = a.strips[uniform(sp.first_strip)];
+            rw_stager<LOCAL>(a, a.masks + uniform64(s0.mask_off) * 4, (int64_t)uniform(s0.nsteps) * 4, req, swin, lane);
+        }
+        return;
+    }
     PairDesc pd = a.pairs[p];
     const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
     const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
@@ -455,6 +537,7 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
         int b = (i - 1) >> 6, k = (i - 1) & 63, jc = j;
         int nrec = 0;
         int pfb = 0, pfclo = INT_MIN;
+        int reqSeq = 0, reqO = 0;  // the last request to the stager
         Lines L;
         // expected column drift of the path per strip (prefetch placement)
         const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
@@ -470,16 +553,47 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
             asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
             uint32_t W[8];
             int jo = jc;
+            int u0 = 0;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             const uint64_t c0 = __builtin_amdgcn_s_memtime();
-#endif
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             tLoadStart += c0;
             ++nStrips;
-            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, sdbg);
-#else
-            rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W);
 #endif
+            // the stager's windows for this strip: origin reqO, entry jc at window (d >> 4), pair d & 15
+            const int d = reqO - jc;
+            if (reqSeq > 0 && d >= 0 && d < 16 * (kStageWin - 8) && uniform(((volatile int *)req)[3]) == reqSeq)
+            {
+                const uint32_t *src = swin[reqSeq & 1] + (d >> 4) * kWave + lane;
+                sfor<8>([&](auto Wc) {
+                    constexpr int w = decltype(Wc)::value;
+                    W[w] = src[w * kWave];
+                });
+                jo = reqO - 16 * (d >> 4);
+                u0 = 2 * (d & 15);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+                ++sdbg[1];  // (counted as staged by the stager)
+#endif
+            }
+            else
+            {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
+                rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, sdbg);
+#else
+                rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W);
+#endif
+            }
+            // the next strip's windows: the stager builds them while this strip is walked
+            if (b > 0 && a.stager)
+            {
+                ++reqSeq;
+                reqO = jc;
+                if (lane == 0)
+                {
+                    ((volatile int *)req)[1] = b - 1;
+                    ((volatile int *)req)[2] = reqO;
+                    ((volatile int *)req)[0] = reqSeq;
+                }
+            }
             // the windows are complete before the prefetch below is issued: otherwise the wait for
             // the staging loads (vmcnt) would also wait for the prefetch
             asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
@@ -498,7 +612,7 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
                 });
                 pfnext = clo;
             }
-            L.u = 0;
+            L.u = u0;
             L.pa = 0;
             L.na = 0;
             L.kk = k;
@@ -582,6 +696,7 @@ __global__ __launch_bounds__(64) void walk_rw_kernel(WalkArgs a)
     }
     if (lane == 0)
     {
+        ((volatile int *)req)[0] = -1;  // the stager quits (every path of the walker ends here)
         a.heads[p] = h;
         if (a.timing)
         {
@@ -964,7 +1079,7 @@ void launch_walk_m(int R, const WalkArgs &a, int np, hipStream_t st)
 {
     switch (R)
     {
-    case 1: hipLaunchKernelGGL(walk_rw_kernel<LOCAL>, dim3(np), dim3(kWave), 0, st, a); break;
+    case 1: hipLaunchKernelGGL(walk_rw_kernel<LOCAL>, dim3(np), dim3(2 * kWave), 0, st, a); break;
     case 2: hipLaunchKernelGGL((walk_cw_kernel<2, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
     case 4: hipLaunchKernelGGL((walk_cw_kernel<4, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
     case 8: hipLaunchKernelGGL((walk_cw_kernel<8, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;

@@ -8,5 +8,7 @@ SA_IO_PROBE=0 bash tools/timeline.sh -l base -m 32768 -o "0 1" -f "$F" || exit 1
 for w in headline local; do
   timeout -k 10 200 python bench.py --workload $w --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/b2_$w.json 2> gpurun_out/b2_$w.err || { tail -n 20 gpurun_out/b2_$w.err; exit 1; }
   python tools/show_bench.py gpurun_out/b2_$w.json
+  SA_TB_STAGER=0 timeout -k 10 200 python bench.py --workload $w --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/b2_${w}_nostager.json 2> gpurun_out/b2_$w.err || { tail -n 20 gpurun_out/b2_$w.err; exit 1; }
+  python tools/show_bench.py gpurun_out/b2_${w}_nostager.json
 done
-bash tools/profile.sh headline_b2 --no-cpu-baseline --steps 5 --warmup 1
+bash tools/profile_all.sh b2
