@@ -713,7 +713,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             mask_entries += (uint64_t)nsteps * R;
             s.bnd_in = b > 0 ? pl->strips.back().bnd_out : 0;
             s.bnd_out = granules;
-            if (b + 1 < ns) granules += n + 8;
+            if (b + 1 < ns) granules += (n + 9) & ~(uint64_t)1;  // even: 16-byte granule pairs (sa_fill.hip)
             pl->strips.push_back(s);
         }
     }
@@ -776,7 +776,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                     bd.mask_off = 0;
                     bd.bnd_in = b > 0 ? pl->bands.back().bnd_out : 0;
                     bd.bnd_out = granules;
-                    granules += n + 8;
+                    granules += (n + 9) & ~(uint64_t)1;
                     pl->bands.push_back(bd);
                 }
                 for (int k = 0; k < d.num_strips; ++k)
