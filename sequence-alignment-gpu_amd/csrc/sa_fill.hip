@@ -1062,9 +1062,12 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     // text codes: kBandAhead bodies ahead (the band step measured 7 % faster with cache-resident codes
-    // than with loads two bodies ahead: their latency is longer behind the drain wave's stores), in
-    // 2 kBandAhead buffers that rotate with the body's place in its loop trip of 2 kBandAhead bodies
-    constexpr int AH = kBandAhead, NB = 2 * kBandAhead;
+    // than with loads two bodies ahead: their latency grows behind the drain wave's stores), in NB =
+    // kBandAhead + 1 buffers that rotate with the body's place in its loop trip of NB bodies; the last
+    // bodies of a strip (fewer than a trip) run one at a time, shifting the buffers down after each
+    // (a compact loop: a fully unrolled remainder doubled the band loop's code, and local bands, whose
+    // code is the largest, measured 13 % slower with it)
+    constexpr int AH = kBandAhead, NB = kBandAhead + 1;
     int T[NB][2][4];
     sfor<AH>([&](auto Kc) {
         constexpr int k = decltype(Kc)::value;
@@ -1119,60 +1122,35 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         F0 = r.F0;
         F1 = r.F1;
         feed(s1, FULL);
-        if constexpr ((POS & 3) == 3) consumed(s1 + U);
+        if constexpr (POS == NB - 1) consumed(s1 + U);
     };
     const int nSteps = sd.nsteps;  // a multiple of 2U
     int s0 = 0;
-    // loop trips of NB bodies up to `end` (a multiple of 2U), then the remaining pairs of bodies,
-    // after which the buffers rotate back so that the next trip starts with buffer 0 (once per phase)
-    auto phase = [&](auto full, int end) __attribute__((always_inline)) {
-        for (; s0 + (NB - 1) * U < end; s0 += NB * U)
-        {
-            set_trip(s0);
-            sfor<NB>([&](auto Pc) { body(Pc, full, s0 + decltype(Pc)::value * U); });
-        }
-        const int rem = (end - s0) / U;  // 0, 2, ..., NB - 2 bodies
-        if (rem > 0)
-        {
-            set_trip(s0);
-            sfor<NB / 2 - 1>([&](auto Hc) {
-                constexpr int h = decltype(Hc)::value;
-                if (2 * h < rem)
-                {
-                    body(std::integral_constant<int, 2 * h>{}, full, s0 + 2 * h * U);
-                    body(std::integral_constant<int, 2 * h + 1>{}, full, s0 + (2 * h + 1) * U);
-                }
+    // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered): whole trips
+    const int endFull = min(nSteps, max(0, (n - U) / (NB * U) * (NB * U)));
+    for (; s0 < endFull; s0 += NB * U)
+    {
+        set_trip(s0);
+        sfor<NB>([&](auto Pc) { body(Pc, std::true_type{}, s0 + decltype(Pc)::value * U); });
+    }
+    for (; s0 + (NB - 1) * U < nSteps; s0 += NB * U)
+    {
+        set_trip(s0);
+        sfor<NB>([&](auto Pc) { body(Pc, std::false_type{}, s0 + decltype(Pc)::value * U); });
+    }
+    for (; s0 < nSteps; s0 += U)
+    {
+        set_trip(s0);
+        body(std::integral_constant<int, 0>{}, std::false_type{}, s0);
+        sfor<NB - 1>([&](auto Kc) {
+            constexpr int k = decltype(Kc)::value;
+            sfor<4>([&](auto Qc) {
+                constexpr int q = decltype(Qc)::value;
+                T[k][0][q] = T[k + 1][0][q];
+                T[k][1][q] = T[k + 1][1][q];
             });
-            s0 += rem * U;
-            // the next AH bodies' codes are in buffers rem .. rem + AH - 1 (mod NB)
-            sfor<NB / 2 - 1>([&](auto Hc) {
-                constexpr int sh = 2 * (decltype(Hc)::value + 1);
-                if (rem == sh)
-                {
-                    int X[AH][2][4];
-                    sfor<AH>([&](auto Bc) {
-                        constexpr int k = decltype(Bc)::value;
-                        sfor<4>([&](auto Qc) {
-                            constexpr int q = decltype(Qc)::value;
-                            X[k][0][q] = T[(k + sh) % NB][0][q];
-                            X[k][1][q] = T[(k + sh) % NB][1][q];
-                        });
-                    });
-                    sfor<AH>([&](auto Bc) {
-                        constexpr int k = decltype(Bc)::value;
-                        sfor<4>([&](auto Qc) {
-                            constexpr int q = decltype(Qc)::value;
-                            T[k][0][q] = X[k][0][q];
-                            T[k][1][q] = X[k][1][q];
-                        });
-                    });
-                }
-            });
-        }
-    };
-    // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered), then the rest
-    phase(std::true_type{}, min(nSteps, max(0, (n - U) / (2 * U) * (2 * U))));
-    phase(std::false_type{}, nSteps);
+        });
+    }
     if (a.timeline && lane == 0)
     {
         // band records follow the strips' (kTimelineWords words each)
