@@ -196,8 +196,10 @@ struct Knobs {
                                     // default: on wherever it applies (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
-    int io_probe = 1;               // SA_IO_PROBE: 0 = full-window polls while a group waits for its
-                                    // first column too
+    int io_probe = 0;               // SA_IO_PROBE=1: while a group waits for its first column, poll
+                                    // one granule (measured: no gain in the band step, and the first
+                                    // hand-off of every group one round trip later, cross-group lag
+                                    // 3.09 -> 3.44 us, profiles/r04/timeline_ablations_v2.log)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
     const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
