@@ -85,19 +85,24 @@ constexpr int kRingMask = kRing - 1;
 #ifndef SA_FILL_ASM
 #define SA_FILL_ASM 1
 #endif
+#ifndef SA_BAND_AHEAD
+#define SA_BAND_AHEAD 4
+#endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_BAND_AHEAD) || \
+    defined(SA_EXP_GRANULE8)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
 #define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
+#define SA_BAND_AHEAD 4  // bands: text-code loads this many bodies ahead
 #endif
 constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer resource, dword 3 (no format, no swizzle)
 constexpr int kAuxSc1 = 16;                // buffer access cache policy: sc1 (agent-coherent, as the granules)
 constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
-constexpr int kBandAhead = 4;  // bands: text-code loads run four bodies ahead (trips of eight bodies)
+constexpr int kBandAhead = SA_BAND_AHEAD;  // bands: text-code loads run this many bodies ahead
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
@@ -164,6 +169,11 @@ constexpr int kConsEvery = 256;  // a consumer publishes its consumption word ev
 // of column c0 (16-byte aligned: granule arrays start at even indices and windows at even counts).
 __device__ __forceinline__ void store_granule_pairs(uint64_t *base, int x, int lane, bool active, uint32_t epoch)
 {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_GRANULE8)
+    // ablation: one 8-byte store per column (round 3's granule stores)
+    if (active) store_granule(base + lane, ((uint64_t)epoch << 32) | (uint32_t)x);
+    return;
+#endif
     const int y = __builtin_amdgcn_mov_dpp(x, 0x101, 0xf, 0xf, false);  // row_shl:1: lane l <- lane l + 1
     if ((lane & 1) == 0 && active)
     {
