@@ -91,8 +91,7 @@ constexpr int kRingMask = kRing - 1;
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_BAND_AHEAD) || \
-    defined(SA_EXP_GRANULE8)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_BAND_AHEAD)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -160,29 +159,15 @@ __device__ __forceinline__ int ring_tag_raw(int c) { return (int)((uint32_t)(c +
 static_assert(kRing == 2048, "ring_tag assumes 2048-entry rings");
 constexpr int kConsEvery = 256;  // a consumer publishes its consumption word every this many columns
 
-// Granule stores of a drained window (lane l holds column c0 + l, c0 odd, as its untagged value x;
-// `active`: the lane's column is to be stored). Columns go out in pairs (c, c + 1), c odd, as ONE
-// 16-byte write-through store {x_c, epoch, x_c+1, epoch} by the even lane: its two 8-byte halves are
-// exactly the two columns' granules, so readers still load one 8-byte granule per column. A 16-byte
-// sc1 store costs about what a plain store does and an 8-byte one 2.7x per byte (MI355X_MICROARCH.md),
-// and these stores share the CU's memory pipeline with the bands' text-code loads. base = the granule
-// of column c0 (16-byte aligned: granule arrays start at even indices and windows at even counts).
-__device__ __forceinline__ void store_granule_pairs(uint64_t *base, int x, int lane, bool active, uint32_t epoch)
+// Granule stores of a drained window: lane l holds column c0 + l as its untagged value x, `active`
+// when the column is to be stored; base = the granule of column c0. One 8-byte write-through store per
+// column. (Pairs of columns as one 16-byte store each, whose halves are the two granules, measured
+// slower end to end: same-box A/B 1.200 vs 1.224 ms at 32768^2, the hand-off lags grew more than the
+// cheaper stores saved, profiles/r04/ab_granule_ahead_v1.log.)
+__device__ __forceinline__ void store_granules(uint64_t *base, int x, int lane, bool active, uint32_t epoch)
 {
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_GRANULE8)
-    // ablation: one 8-byte store per column (round 3's granule stores)
     if (active) store_granule(base + lane, ((uint64_t)epoch << 32) | (uint32_t)x);
-    return;
-#endif
-    const int y = __builtin_amdgcn_mov_dpp(x, 0x101, 0xf, 0xf, false);  // row_shl:1: lane l <- lane l + 1
-    if ((lane & 1) == 0 && active)
-    {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, kBufRsrcWord3);
-        __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)x, epoch, (uint32_t)y, epoch}, rs, (uint32_t)lane * 8u, 0, kAuxSc1);
-    }
 }
-constexpr int kIoWin = 4;        // I/O wave: 64-column windows polled / drained per round
-
 
 // a + sign_extend(byte B of w), one VALU op
 template <int B>
@@ -1438,9 +1423,8 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
             const int x = lds_ld(rl + ring_slot(c)) ^ ring_tag(c);
             const uint64_t rdy = ballot(x >= 0 && c <= nOut);
             int upto = drained + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
-            if (upto < nOut) upto = drained + ((upto - drained) & ~1);  // whole column pairs (16-B granules)
             if (!(upto - drained >= 16 || (upto >= nOut && upto > drained))) break;
-            store_granule_pairs(bout + drained, x, lane, c <= upto, a.epoch);
+            store_granules(bout + drained, x, lane, c <= upto, a.epoch);
             const bool full = upto - drained == kWave;
             drained = upto;
             if (lane == 0)
@@ -1546,9 +1530,8 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
                     const int x = lds_ld(rings + (r + 1) * kRing + ring_slot(c)) ^ ring_tag(c);
                     const uint64_t rdy = ballot(x >= 0 && c <= drN[r]);
                     int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
-                    if (upto < drN[r]) upto = dr[r] + ((upto - dr[r]) & ~1);  // whole column pairs
                     if (!(upto - dr[r] >= 16 || (upto >= drN[r] && upto > dr[r]))) break;
-                    store_granule_pairs(drOut[r] + dr[r], x, lane, c <= upto, a.epoch);
+                    store_granules(drOut[r] + dr[r], x, lane, c <= upto, a.epoch);
                     const bool full = upto - dr[r] == kWave;
                     dr[r] = upto;
                     if (lane == 0) lds_st((lds_int *)&drain[r + 1], upto);
