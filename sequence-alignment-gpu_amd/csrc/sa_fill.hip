@@ -169,6 +169,8 @@ __device__ __forceinline__ void store_granules(uint64_t *base, int x, int lane, 
     if (active) store_granule(base + lane, ((uint64_t)epoch << 32) | (uint32_t)x);
 }
 
+constexpr int kIoWin = 4;        // I/O wave: 64-column windows polled / drained per round
+
 // a + sign_extend(byte B of w), one VALU op
 template <int B>
 __device__ __forceinline__ int add_sbyte(int a, int w)
