@@ -196,10 +196,6 @@ struct Knobs {
                                     // default: on wherever it applies (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
-    int io_probe = 0;               // SA_IO_PROBE=1: while a group waits for its first column, poll
-                                    // one granule (measured: no gain in the band step, and the first
-                                    // hand-off of every group one round trip later, cross-group lag
-                                    // 3.09 -> 3.44 us, profiles/r04/timeline_ablations_v2.log)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
     const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
@@ -219,7 +215,6 @@ const Knobs &knobs()
         if (const char *e = get("SA_BAND")) v.band = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_HANDOFF_TIMEOUT_S")) v.handoff_timeout_s = std::atof(e);
         if (const char *e = get("SA_IO_SLEEP")) v.io_sleep = std::max(0, std::atoi(e));
-        if (const char *e = get("SA_IO_PROBE")) v.io_probe = std::atoi(e) != 0 ? 1 : 0;
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
         v.timeline = get("SA_TIMELINE");
         v.tb_timing = get("SA_TB_TIMING");
@@ -715,7 +710,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             mask_entries += (uint64_t)nsteps * R;
             s.bnd_in = b > 0 ? pl->strips.back().bnd_out : 0;
             s.bnd_out = granules;
-            if (b + 1 < ns) granules += (n + 9) & ~(uint64_t)1;  // even: 16-byte granule pairs (sa_fill.hip)
+            if (b + 1 < ns) granules += n + 8;
             pl->strips.push_back(s);
         }
     }
@@ -778,7 +773,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                     bd.mask_off = 0;
                     bd.bnd_in = b > 0 ? pl->bands.back().bnd_out : 0;
                     bd.bnd_out = granules;
-                    granules += (n + 9) & ~(uint64_t)1;
+                    granules += n + 8;
                     pl->bands.push_back(bd);
                 }
                 for (int k = 0; k < d.num_strips; ++k)
@@ -975,7 +970,6 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.key_rowbits = pl->key_rowbits;
         a.timeout_ticks = (uint64_t)(knobs().handoff_timeout_s * 1e8);
         a.io_sleep = knobs().io_sleep;
-        a.io_probe = knobs().io_probe;
         a.chain_lds = knobs().chain_lds_kb * 1024;
         a.bands = pl->d_bands;
         a.num_bands = 0;

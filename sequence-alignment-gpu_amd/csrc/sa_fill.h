@@ -32,7 +32,6 @@ struct FillArgs {
     uint64_t timeout_ticks;     // hand-off give-up time in s_memrealtime ticks (100 MHz)
     uint64_t *timeline;         // debug (SA_TIMELINE): per strip {start, fed, end, hw id}, or null
     int32_t io_sleep;           // I/O wave idle poll period, in units of s_sleep 1 (64 clocks)
-    int32_t io_probe;           // I/O wave: probe one granule while a group waits for its first column
     int32_t chain_lds;          // chain launches: dynamic LDS bytes (>= group_lds_bytes(W); more
                                 // than half a CU's LDS keeps one workgroup per CU)
     // BAND fill (R = 1 int8-profile chains, sa_fill.hip process_band): 128-row score strips (bands)

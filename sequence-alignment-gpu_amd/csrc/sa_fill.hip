@@ -85,23 +85,18 @@ constexpr int kRingMask = kRing - 1;
 #ifndef SA_FILL_ASM
 #define SA_FILL_ASM 1
 #endif
-#ifndef SA_BAND_AHEAD
-#define SA_BAND_AHEAD 4
-#endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_BAND_AHEAD)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
 #define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
-#define SA_BAND_AHEAD 4  // bands: text-code loads this many bodies ahead
 #endif
 constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer resource, dword 3 (no format, no swizzle)
 constexpr int kAuxSc1 = 16;                // buffer access cache policy: sc1 (agent-coherent, as the granules)
 constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
-constexpr int kBandAhead = SA_BAND_AHEAD;  // bands: text-code loads run this many bodies ahead
 
 struct GroupHdr {
     int S[32 * 32];                // generic score table (A <= 32)
@@ -158,18 +153,8 @@ __device__ __forceinline__ int ring_tag(int c) { return (int)((((uint32_t)(c + 6
 __device__ __forceinline__ int ring_tag_raw(int c) { return (int)((uint32_t)(c + 63) << 20); }
 static_assert(kRing == 2048, "ring_tag assumes 2048-entry rings");
 constexpr int kConsEvery = 256;  // a consumer publishes its consumption word every this many columns
-
-// Granule stores of a drained window: lane l holds column c0 + l as its untagged value x, `active`
-// when the column is to be stored; base = the granule of column c0. One 8-byte write-through store per
-// column. (Pairs of columns as one 16-byte store each, whose halves are the two granules, measured
-// slower end to end: same-box A/B 1.200 vs 1.224 ms at 32768^2, the hand-off lags grew more than the
-// cheaper stores saved, profiles/r04/ab_granule_ahead_v1.log.)
-__device__ __forceinline__ void store_granules(uint64_t *base, int x, int lane, bool active, uint32_t epoch)
-{
-    if (active) store_granule(base + lane, ((uint64_t)epoch << 32) | (uint32_t)x);
-}
-
 constexpr int kIoWin = 4;        // I/O wave: 64-column windows polled / drained per round
+
 
 // a + sign_extend(byte B of w), one VALU op
 template <int B>
@@ -1058,18 +1043,9 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     int msbv;
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
-    // text codes: kBandAhead bodies ahead (the band step measured 7 % faster with cache-resident codes
-    // than with loads two bodies ahead: their latency grows behind the drain wave's stores), in NB =
-    // kBandAhead + 1 buffers that rotate with the body's place in its loop trip of NB bodies; the last
-    // bodies of a strip (fewer than a trip) run one at a time, shifting the buffers down after each
-    // (a compact loop: a fully unrolled remainder doubled the band loop's code, and local bands, whose
-    // code is the largest, measured 13 % slower with it)
-    constexpr int AH = kBandAhead, NB = kBandAhead + 1;
-    int T[NB][2][4];
-    sfor<AH>([&](auto Kc) {
-        constexpr int k = decltype(Kc)::value;
-        load_codes(k * U, T[k][0], T[k][1]);
-    });
+    int TA0[4], TA1[4], TB0[4], TB1[4], TC0[4], TC1[4], TD0[4], TD1[4];
+    load_codes(0, TA0, TA1);
+    load_codes(U, TB0, TB1);
     if constexpr (HP)
     {
         int c = 1 + lane;
@@ -1079,16 +1055,16 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     feed(0, false);
     const uint64_t tFed = a.timeline ? now_ticks() : 0;
     const uint64_t cFed = a.timeline ? __builtin_amdgcn_s_memtime() : 0;
-    uint32_t tripPf = 0;
-    auto set_trip = [&](int s0t) __attribute__((always_inline)) {
-        tripPf = 4u * (uint32_t)s0t + 4u * (U + 64);
-        asm volatile("" : "+s"(tripPf));
+    uint32_t quadPf = 0;
+    auto set_quad = [&](int s0q) __attribute__((always_inline)) {
+        quadPf = 4u * (uint32_t)s0q + 4u * (U + 64);
+        asm volatile("" : "+s"(quadPf));
     };
-    auto body = [&](auto pos, auto full, int s0) __attribute__((always_inline)) {
+    auto body = [&](auto pos, auto full, int s0, int (&T0)[4], int (&T1)[4], int (&Tn0)[4], int (&Tn1)[4]) __attribute__((always_inline)) {
         constexpr int POS = decltype(pos)::value;
         constexpr bool FULL = decltype(full)::value;
         const int s1 = s0 + U;
-        load_codes(s0 + AH * U, T[(POS + AH) % NB][0], T[(POS + AH) % NB][1]);
+        load_codes(s0 + 2 * U, Tn0, Tn1);
         BandRegs r;
         r.Q = Q;
         r.diag = diag;
@@ -1096,15 +1072,15 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         r.F1 = F1;
         sfor<4>([&](auto Wc) {
             constexpr int q = decltype(Wc)::value;
-            r.TA[q] = T[POS][0][q];
-            r.TB[q] = T[POS][1][q];
+            r.TA[q] = T0[q];
+            r.TB[q] = T1[q];
         });
         r.g = a.gap;
-        r.pfaddr = HP ? (int)(rinLaneOff + ((tripPf + 4u * U * POS) & (4u * kRingMask))) : 0;
+        r.pfaddr = HP ? (int)(rinLaneOff + ((quadPf + 4u * U * POS) & (4u * kRingMask))) : 0;
         r.ctag = ring_tag_raw(s1 + 1);
         r.msb = msbv;
-        // one backpressure check per two bodies (this one and the next)
-        if constexpr ((POS & 1) == 0) pub_wait(s0 + U);
+        if constexpr (POS == 0) pub_wait(s0 + 3 * U);
+        else if constexpr (POS == 2) pub_wait(s0 + U);
         r.pubaddr = (int)lds_off(pubBase + (s0 & kRingMask));
         r.pubtag = ring_tag_raw(s0 - 63);
         band_steps_asm<LOCAL, HN, HP>(r);
@@ -1119,35 +1095,42 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         F0 = r.F0;
         F1 = r.F1;
         feed(s1, FULL);
-        if constexpr (POS == NB - 1) consumed(s1 + U);
+        if constexpr (POS == 3) consumed(s1 + U);
     };
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
     const int nSteps = sd.nsteps;  // a multiple of 2U
     int s0 = 0;
-    // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered): whole trips
-    const int endFull = min(nSteps, max(0, (n - U) / (NB * U) * (NB * U)));
-    for (; s0 < endFull; s0 += NB * U)
-    {
-        set_trip(s0);
-        sfor<NB>([&](auto Pc) { body(Pc, std::true_type{}, s0 + decltype(Pc)::value * U); });
-    }
-    for (; s0 + (NB - 1) * U < nSteps; s0 += NB * U)
-    {
-        set_trip(s0);
-        sfor<NB>([&](auto Pc) { body(Pc, std::false_type{}, s0 + decltype(Pc)::value * U); });
-    }
-    for (; s0 < nSteps; s0 += U)
-    {
-        set_trip(s0);
-        body(std::integral_constant<int, 0>{}, std::false_type{}, s0);
-        sfor<NB - 1>([&](auto Kc) {
-            constexpr int k = decltype(Kc)::value;
+    // quads of bodies up to `end` (a multiple of 2U), then at most one pair (process_strip's phases)
+    auto phase = [&](auto full, int end) __attribute__((always_inline)) {
+        for (; s0 + 2 * U < end; s0 += 4 * U)
+        {
+            set_quad(s0);
+            body(P0{}, full, s0, TA0, TA1, TC0, TC1);
+            body(P1{}, full, s0 + U, TB0, TB1, TD0, TD1);
+            body(P2{}, full, s0 + 2 * U, TC0, TC1, TA0, TA1);
+            body(P3{}, full, s0 + 3 * U, TD0, TD1, TB0, TB1);
+        }
+        if (s0 < end)
+        {
+            set_quad(s0 - 2 * U);
+            body(P2{}, full, s0, TA0, TA1, TC0, TC1);
+            body(P3{}, full, s0 + U, TB0, TB1, TD0, TD1);
+            s0 += 2 * U;
             sfor<4>([&](auto Qc) {
                 constexpr int q = decltype(Qc)::value;
-                T[k][0][q] = T[k + 1][0][q];
-                T[k][1][q] = T[k + 1][1][q];
+                TA0[q] = TC0[q];
+                TA1[q] = TC1[q];
+                TB0[q] = TD0[q];
+                TB1[q] = TD1[q];
             });
-        });
-    }
+        }
+    };
+    // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered), then the rest
+    phase(std::true_type{}, min(nSteps, max(0, (n - U) / (2 * U) * (2 * U))));
+    phase(std::false_type{}, nSteps);
     if (a.timeline && lane == 0)
     {
         // band records follow the strips' (kTimelineWords words each)
@@ -1400,33 +1383,22 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
             want = min(min(kIoWin * kWave, nIn - copied), room);
             if (want < min(16, nIn - copied)) want = 0;
         }
-        // polls load whole windows (one round trip from the producer's store to the ring; a lane-0
-        // probe first would add a second), except while the group waits for its first column (up to
-        // hundreds of microseconds for the late groups of a band launch, all polling at once): then
-        // lane 0 probes that column's 8 bytes, and the first full poll follows its match
-        const bool probe = a.io_probe && copied == 0;
+        // every poll loads whole windows (one round trip from the producer's store to the ring; a
+        // lane-0 probe first would add a second): a few KiB per poll per waiting group is nothing
+        // next to the fill's own traffic
         sfor<kIoWin>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
-            v[q] = q * kWave + lane < (probe ? 1 : want) ? load_granule(bin + copied + q * kWave + lane) : 0;
+            v[q] = q * kWave + lane < want ? load_granule(bin + copied + q * kWave + lane) : 0;
         });
-        if (probe && want > 0 && uniform((int)((uint32_t)(v[0] >> 32) == a.epoch)) == 0)
-            want = -1;  // nothing yet: no copy this round (the drain below still runs)
-        else if (probe && want > 0)
-        {
-            sfor<kIoWin>([&](auto Qc) {
-                constexpr int q = decltype(Qc)::value;
-                v[q] = q * kWave + lane < want ? load_granule(bin + copied + q * kWave + lane) : 0;
-            });
-        }
         // 2. drain ring[W'] into granules for the next group (up to kIoWin windows)
         for (int rep = 0; rep < kIoWin && drained < nOut; ++rep)
         {
             const int c = drained + lane + 1;
             const int x = lds_ld(rl + ring_slot(c)) ^ ring_tag(c);
             const uint64_t rdy = ballot(x >= 0 && c <= nOut);
-            int upto = drained + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
+            const int upto = drained + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
             if (!(upto - drained >= 16 || (upto >= nOut && upto > drained))) break;
-            store_granules(bout + drained, x, lane, c <= upto, a.epoch);
+            if (c <= upto) store_granule(bout + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
             const bool full = upto - drained == kWave;
             drained = upto;
             if (lane == 0)
@@ -1440,7 +1412,6 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
         // 3. the poll's result -> ring[0]
         int total = 0;  // ready prefix over the windows
         bool open = want > 0;
-        if (want < 0) want = 0;
         sfor<kIoWin>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
             if (!open) return;
@@ -1531,9 +1502,9 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
                     const int c = dr[r] + lane + 1;
                     const int x = lds_ld(rings + (r + 1) * kRing + ring_slot(c)) ^ ring_tag(c);
                     const uint64_t rdy = ballot(x >= 0 && c <= drN[r]);
-                    int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
+                    const int upto = dr[r] + (~rdy == 0 ? kWave : (int)__builtin_ctzll(~rdy));
                     if (!(upto - dr[r] >= 16 || (upto >= drN[r] && upto > dr[r]))) break;
-                    store_granules(drOut[r] + dr[r], x, lane, c <= upto, a.epoch);
+                    if (c <= upto) store_granule(drOut[r] + c - 1, ((uint64_t)a.epoch << 32) | (uint32_t)x);
                     const bool full = upto - dr[r] == kWave;
                     dr[r] = upto;
                     if (lane == 0) lds_st((lds_int *)&drain[r + 1], upto);
