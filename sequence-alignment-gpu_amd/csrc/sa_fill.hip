@@ -85,15 +85,20 @@ constexpr int kRingMask = kRing - 1;
 #ifndef SA_FILL_ASM
 #define SA_FILL_ASM 1
 #endif
+#ifndef SA_DRAIN_WAVES
+#define SA_DRAIN_WAVES 3
+#endif
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_DRAIN_WAVES)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
 #define SA_FILL_ASM 1  // hand-scheduled steady steps (0: the compiler-scheduled run_body)
+#define SA_DRAIN_WAVES 3  // band workgroups: drain waves (one per in-group ring, so one per band SIMD)
 #endif
+constexpr int kDrainWaves = SA_DRAIN_WAVES;
 constexpr int kBufRsrcWord3 = 0x00020000;  // gfx9 raw buffer resource, dword 3 (no format, no swizzle)
 constexpr int kAuxSc1 = 16;                // buffer access cache policy: sc1 (agent-coherent, as the granules)
 constexpr int kCodeAhead = 2;  // R = 1: text-code loads run two bodies ahead (bodies in quads)
@@ -1463,7 +1468,11 @@ __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *stri
 // still drains the last ring. A wave of its own: its write-through stores would otherwise sit in the
 // I/O wave's vmcnt in front of every granule poll (in-order completion) and slow the cross-group
 // hand-off.
-__device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_int *rings, int grp, int W, int lane)
+// With kDrainWaves drain waves, wave d copies the rings r + 1 with r = d (mod kDrainWaves): with three,
+// one ring each, and every SIMD of the workgroup holds one band and one helper wave (the I/O wave or a
+// drain wave) instead of one SIMD carrying all three rings' copies beside its band, whose pace the
+// whole chain then takes.
+__device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_int *rings, int grp, int W, int lane, int d)
 {
     const int first = grp * W;
     const int last = min(first + W, a.num_bands) - 1;
@@ -1476,7 +1485,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
         dr[r] = 0;
         drN[r] = 0;
         drOut[r] = a.bnd;
-        if (r + 1 < wl)
+        if (r + 1 < wl && r % kDrainWaves == d)
         {
             const StripDesc sr = a.bands[first + r];
             if (uniform(sr.flags) & kHasNext)
@@ -1523,7 +1532,8 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
         if ((spin & 127) == 0 && !keep_waiting(a, t0, lane))
         {
             if (lane == 0)
-                for (int r = 1; r < wl; ++r) lds_st((lds_int *)&drain[r], 1 << 30);  // release the producers
+                for (int r = 1; r < wl; ++r)
+                    if ((r - 1) % kDrainWaves == d) lds_st((lds_int *)&drain[r], 1 << 30);  // release the producers
             return;
         }
     }
@@ -1533,7 +1543,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
 template <int R, bool LOCAL, int SK, bool CHAIN>
-__global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs a)
+__global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
     GroupHdr &H = *reinterpret_cast<GroupHdr *>(lds_dyn);
@@ -1543,7 +1553,7 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
     // compute waves; with CHAIN wave W is the I/O wave (plans without strip chains have none, and no
     // rings in LDS either: more workgroups fit a CU); band launches have one more wave, the drain
     // wave W + 1 (idle in the strip workgroups)
-    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0) - (CHAIN && a.num_bands > 0 ? 1 : 0);
+    const int W = (int)(blockDim.x / kWave) - (CHAIN ? 1 : 0) - (CHAIN && a.num_bands > 0 ? kDrainWaves : 0);
     if constexpr (SK == kTable)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) H.S[e] = a.score_tab[e];
     // BAND fill: workgroups [0, band_wgs) take groups of W bands from their own queue, the others
@@ -1581,14 +1591,14 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 2)) void fill_kernel(FillArgs 
         {
             io_wave(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane);
         }
-        else if (CHAIN && w == W + 1)
+        else if (CHAIN && w > W)
         {
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_DRAIN)
             // timing ablation: no copies of the in-group rings to granules (the strips starve)
             if (bandRole && lane == 0)
                 for (int r = 1; r <= W; ++r) lds_st((lds_int *)&H.drain[r], 1 << 30);
 #else
-            if (bandRole) drain_wave(a, H.drain, rings, grp, W, lane);
+            if (bandRole) drain_wave(a, H.drain, rings, grp, W, lane, w - W - 1);
 #endif
         }
         else
@@ -1649,7 +1659,7 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1 + (a.num_bands > 0 ? 1 : 0))), lds, st, a);
+        hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true>), dim3(grid), dim3(kWave * (W + 1 + (a.num_bands > 0 ? kDrainWaves : 0))), lds, st, a);
     }
     else hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, false>), dim3(grid), dim3(kWave * W), sizeof(GroupHdr), st, a);
 }
