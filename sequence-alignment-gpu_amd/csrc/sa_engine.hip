@@ -1043,7 +1043,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     DevPtr<uint64_t> tmBuf;
     if (tmPath)
     {
-        HIP_TRY(hipMalloc((void **)&timing, sizeof(uint64_t) * 8 * np));
+        HIP_TRY(hipMalloc((void **)&timing, sizeof(uint64_t) * 9 * np));
         tmBuf.reset(timing);
     }
     // row / column walk (records) + expansion (sa_walk.hip)
@@ -1083,7 +1083,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     if (int rc = debug_sync(st, "expand_kernel")) return rc;
     if (tmPath)
     {
-        std::vector<uint64_t> tm(8 * (size_t)np);
+        std::vector<uint64_t> tm(9 * (size_t)np);
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMemcpy(tm.data(), timing, tm.size() * 8, hipMemcpyDeviceToHost));
         if (FILE *f = std::fopen(tmPath, "wb"))

@@ -543,7 +543,7 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
         const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
         uint64_t tStage = 0, tBatch = 0;  // shader clocks in staging / in the walk proper
-        uint64_t sdbg[2] = {0, 0}, tLoadStart = 0, nStrips = 0, nRestage = 0;
+        uint64_t sdbg[2] = {0, 0}, tLoadStart = 0, nStrips = 0, nRestage = 0, nStagerHit = 0;
 #endif
         while (b >= 0)
         {
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
                 jo = reqO - 16 * (d >> 4);
                 u0 = 2 * (d & 15);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
-                ++sdbg[1];  // (counted as staged by the stager)
+                ++nStagerHit;
 #endif
             }
             else
@@ -676,6 +676,7 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 1] = sdbg[1];
             a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 2] = nStrips;
             a.timing[4 * (size_t)gridDim.x + 4 * (size_t)p + 3] = nRestage;
+            a.timing[8 * (size_t)gridDim.x + (size_t)p] = nStagerHit;
         }
 #endif
         if (!L.stopped)

@@ -38,5 +38,7 @@ if len(tm) >= 4 and tm[2] > 0:
     if len(tm) >= 8 and tm[6] > 0:
         rec.update({"stage_load_clk_per_strip": round(tm[4] / tm[6], 1), "pf_miss": int(tm[5]),
                     "strips": int(tm[6]), "restages": int(tm[7])})
+    if len(tm) >= 9:
+        rec["stager_hits"] = int(tm[8])  # strips whose windows came from the stager wave
 print(rec)
 b.close()
