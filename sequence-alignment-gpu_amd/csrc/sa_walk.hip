@@ -598,9 +598,10 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             // the staging loads (vmcnt) would also wait for the prefetch
             asm volatile("" : "+v"(W[0]), "+v"(W[1]), "+v"(W[2]), "+v"(W[3]), "+v"(W[4]), "+v"(W[5]), "+v"(W[6]), "+v"(W[7]));
             int pfnext = INT_MIN;
-            if (b > 0)
+            if (b > 0 && !a.stager)
             {
-                // raw planes of the strip above around the predicted entry column -> LDS
+                // raw planes of the strip above around the predicted entry column -> LDS (without the
+                // stager wave; with it, the rare strip it does not cover is staged from global memory)
                 const int pred = jc - drift;
                 const int clo = max(0, min((pred - 225) >> 5, nchunks - kPfChunks));
                 const uint32_t *src = sb - sstride + (int64_t)clo * kChunkDw;
