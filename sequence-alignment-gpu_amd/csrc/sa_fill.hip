@@ -91,7 +91,8 @@ constexpr int kRingMask = kRing - 1;
 #else
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
-    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_DRAIN_WAVES)
+    defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_DRAIN_WAVES) || \
+    defined(SA_EXP_BAND_STAMPS)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -1101,6 +1102,12 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         F1 = r.F1;
         feed(s1, FULL);
         if constexpr (POS == 3) consumed(s1 + U);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_STAMPS)
+        // timing: when the band finished steps 0..15, 16..31, ..., 64..79 (words 6..10; the body at 64
+        // publishes the first feed of the band below)
+        if (a.timeline && s0 <= 64 && lane == 0)
+            a.timeline[kTimelineWords * ((size_t)a.num_strips + idx) + 6 + s0 / U] = now_ticks();
+#endif
     };
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;
