@@ -92,7 +92,7 @@ constexpr int kRingMask = kRing - 1;
 #if defined(SA_PF_LEAD) || defined(SA_FILL_ASM) || defined(SA_EXP_CODES_CONST) || defined(SA_EXP_NO_STORE) || \
     defined(SA_EXP_NO_FEED_WAIT) || defined(SA_EXP_NODIR) || defined(SA_EXP_NO_MERGE) || defined(SA_EXP_FILL_INC) || \
     defined(SA_EXP_BROW_AUX) || defined(SA_EXP_NO_STRIPS) || defined(SA_EXP_NO_DRAIN) || defined(SA_DRAIN_WAVES) || \
-    defined(SA_EXP_BAND_STAMPS)
+    defined(SA_EXP_BAND_STAMPS) || defined(SA_EXP_BAND_WAIT_SLEEP)
 #error "experiment switches need SA_EXPERIMENT (tools/build_exp.sh)"
 #endif
 #define SA_PF_LEAD 4   // R = 1: steps between a body's feed read and its use (sa_fill_steps.inc matches)
@@ -1006,7 +1006,11 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
                 uint64_t t0 = 0;
                 for (uint32_t spin = 1;; ++spin)
                 {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_WAIT_SLEEP)
+                    if (spin > 16) { for (int z = 0; z < SA_EXP_BAND_WAIT_SLEEP; ++z) __builtin_amdgcn_s_sleep(1); }
+#else
                     if (spin > 16) __builtin_amdgcn_s_sleep(1);
+#endif
                     x = ds_read_sync(rin + lane + ring_slot(base + 1)) ^ tag;
                     if ((ballot(x < 0) & need) == 0) break;
                     if ((spin & 255) == 0)

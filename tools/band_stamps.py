@@ -36,7 +36,8 @@ det = (fed[1:] - body[:-1, 4]) * 10.0
 W = 4
 k = np.arange(1, len(fed))
 ing = (k % W) != 0
-print({"bands": len(fed), "stamped": int(ok.sum()),
+st = tl[:ns]
+print({"total_us": round(float(st[:, 2].max() - tl[:, 0][tl[:, 0] > 0].min()) * 0.01, 1), "bands": len(fed), "stamped": int(ok.sum()),
        "fed_to_body_done_ns": [round(float(x), 1) for x in rel[ok].mean(axis=0)],
        "lag_in_group_ns": round(float(lag[ing].mean()), 1), "lag_cross_ns": round(float(lag[~ing].mean()), 1),
        "first_publish_to_next_fed_in_group_ns": round(float(det[ing & ok[:-1]].mean()), 1),
