@@ -43,7 +43,7 @@ struct FillArgs {
     int32_t band_wgs;
 };
 
-constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..35: experiment progress stamps)
+constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..37: experiment progress stamps)
 constexpr int kMaxWaves = 4;       // compute waves per chain workgroup (+1 I/O wave: 320 threads; one
                                    // compute wave per SIMD: two per SIMD ran 2.2x slower per step)
 constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed batch kernel

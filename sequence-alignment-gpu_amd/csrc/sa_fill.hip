@@ -1104,14 +1104,18 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         diag = r.diag;
         F0 = r.F0;
         F1 = r.F1;
-        feed(s1, FULL);
-        if constexpr (POS == 3) consumed(s1 + U);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_STAMPS)
-        // timing: when the band finished steps 0..15, 16..31, ..., 64..79 (words 6..10; the body at 64
-        // publishes the first feed of the band below)
-        if (a.timeline && s0 <= 64 && lane == 0)
+        // timing: when the band finished bodies 0..15 (words 6..21; the body at 64 publishes the first
+        // feed of the band below) and when the next body's feed was in hand (words 22..37)
+        if (a.timeline && s0 < 16 * U && lane == 0)
             a.timeline[kTimelineWords * ((size_t)a.num_strips + idx) + 6 + s0 / U] = now_ticks();
+        feed(s1, FULL);
+        if (a.timeline && s0 < 16 * U && lane == 0)
+            a.timeline[kTimelineWords * ((size_t)a.num_strips + idx) + 22 + s0 / U] = now_ticks();
+#else
+        feed(s1, FULL);
 #endif
+        if constexpr (POS == 3) consumed(s1 + U);
     };
     using P0 = std::integral_constant<int, 0>;
     using P1 = std::integral_constant<int, 1>;

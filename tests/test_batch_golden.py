@@ -103,7 +103,7 @@ def _free_port() -> int:
     return port
 
 
-def _gpu_worker(rank, world, port, name, count, q):
+def _gpu_worker(rank, world, port, name, count, q, device_rows=False):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -122,6 +122,18 @@ def _gpu_worker(rank, world, port, name, count, q):
                     [p for _, p in pairs], device=0)
     b.fill()
     b.traceback()
+    if device_rows:
+        # the bench's batch path: sa_result rows device to device (sa_plan_copy_results) into a
+        # ceil(count / world)-row buffer, gathered by distributed.gather_device (gloo: via the host)
+        width = (count + world - 1) // world
+        buf = torch.full((width, 4), -1, dtype=torch.int64, device="cuda:0")
+        b.plan.copy_results(buf.data_ptr())
+        torch.cuda.synchronize()
+        out = distributed.gather_device(buf.cpu(), count, world, rank)
+        b.close()
+        q.put(("rank0" if rank == 0 else "rank1", out, []))
+        dist.destroy_process_group()
+        return
     res = b.all_alignments()
     b.close()
     # strings stay on the rank that made them (only the scalar fields travel): check them here
@@ -135,14 +147,17 @@ def _gpu_worker(rank, world, port, name, count, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name,count", [("global", 512), ("local", 256)])
-def test_sharded_batch_hip_engine_world2(eng, name, count):
-    """Sharded batch path with the HIP engine behind it: two gloo ranks, both on device 0."""
+@pytest.mark.parametrize("name,count,device_rows", [("global", 512, False), ("local", 256, False),
+                                                     ("global", 511, True), ("local", 255, True)])
+def test_sharded_batch_hip_engine_world2(eng, name, count, device_rows):
+    """Sharded batch path with the HIP engine behind it: two gloo ranks, both on device 0. With
+    device_rows, the results travel as bench.py's batch sends them (sa_plan_copy_results rows, then
+    distributed.gather_device; odd counts leave rank 1 one row short)."""
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, name, count, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gpu_worker, args=(r, 2, port, name, count, q, device_rows)) for r in range(2)]
     for p in procs:
         p.start()
     msgs = dict((tag, (out, bad)) for tag, out, bad in (q.get(timeout=150) for _ in range(2)))
@@ -151,6 +166,8 @@ def test_sharded_batch_hip_engine_world2(eng, name, count):
         assert p.exitcode == 0
     assert msgs["rank0"][1] == [] and msgs["rank1"][1] == []
     got = msgs["rank0"][0]
+    if device_rows:  # (count, 4) int64 rows in FIELDS order
+        got = [dict(zip(("score", "num_bytes", "start_text", "start_pattern"), map(int, r))) for r in got]
     exp = fixture()[name]["records"]
     bad = [i for i in range(count) if [got[i][k] for k in ("score", "num_bytes", "start_text", "start_pattern")] != exp[i][:4]]
     assert not bad, f"{len(bad)} pairs differ after the gather, first {bad[:5]}"
