@@ -7,6 +7,13 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 src=$root/sequence-alignment-gpu_amd/csrc
 out=/tmp/sa_build_exp/$tag
 mkdir -p "$out"
+# GEN_ENV="SA_GEN_BAND_PF_STEP=14 ..." regenerates the fill steps with those generator settings into a
+# copy of the sources
+if [ -n "$GEN_ENV" ]; then
+  rm -rf "$out/src" && cp -r "$src" "$out/src"
+  env $GEN_ENV SA_GEN_FILL_OUT="$out/src/sa_fill_steps.inc" python3 "$root/tools/gen_fill_asm.py" >/dev/null
+  src=$out/src
+fi
 flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include -I$src -DSA_EXPERIMENT=1 $*"
 # EXP_ONLY="fill_r1 ..." recompiles only those units and takes the others from the product build
 pids=()
