@@ -648,8 +648,17 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         mzv[t] = m;
     });
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
+    // the compiler's vector-memory wait before each steady body is the most conservative over the
+    // paths into the loop: the first trip must see the steady trips' order (TA's loads, TB's, then one
+    // op standing in for the chunk store that precedes every later trip), or it waits one op further
+    // back on every first body of a quad (a load or store issued a body ago); measured in the asm:
+    // vmcnt(2) -> vmcnt(3) on all steady bodies
     load_codes(0, TA);
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (kAhead == 2) load_codes(U, TB);
+    __builtin_amdgcn_sched_barrier(0);
+    int vmPad = 0;
+    if constexpr (kBuf && kAhead == 2) vmPad = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff, 0, 0);
     prefetch(0);
     feed(0, false);
     const uint64_t tFed = a.timeline ? now_ticks() : 0;
@@ -841,6 +850,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         phase(KSteady{}, std::true_type{}, min(sTail, max(0, (n - U) / (2 * U) * (2 * U))));
         phase(KSteady{}, std::false_type{}, sTail);
         phase(KGeneric{}, std::false_type{}, nSteps);
+        asm volatile("" ::"v"(vmPad));
     }
     else
     {
@@ -977,6 +987,11 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     const uint32_t rinLaneOff = lds_off(rin + lane);
     // the feed protocol of process_strip: read after step BAND_PF_STEP, tags checked at the body end
     int Q = 0, diag = 0, F0 = 0, F1 = 0;  // column-0 boundary
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_MISS)
+    // experiment: feed slow-path entries (bodies 0..63 as a mask, all bodies as a count) and polls
+    uint64_t missMask = 0;
+    uint32_t missCount = 0, spinCount = 0, spin0 = 0;
+#endif
     int pfVal = 0;
     bool pfTagged = false;
     uint64_t pfBad = 0;
@@ -1004,8 +1019,19 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
             if (__builtin_expect((full ? bad : (bad & need)) != 0, 0))
             {
                 uint64_t t0 = 0;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_MISS)
+                if (base > 0)
+                {
+                    ++missCount;
+                    if (base / U - 1 < 64) missMask |= 1ull << (base / U - 1);
+                }
+#endif
                 for (uint32_t spin = 1;; ++spin)
                 {
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_MISS)
+                    if (base > 0) ++spinCount;
+                    else ++spin0;
+#endif
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_WAIT_SLEEP)
                     if (spin > 16) { for (int z = 0; z < SA_EXP_BAND_WAIT_SLEEP; ++z) __builtin_amdgcn_s_sleep(1); }
 #else
@@ -1055,6 +1081,9 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     int TA0[4], TA1[4], TB0[4], TB1[4], TC0[4], TC1[4], TD0[4], TD1[4];
     load_codes(0, TA0, TA1);
+    // TA's two loads before TB's, as in the steady quads: otherwise the loop's first body waits for
+    // one of the previous body's loads in every quad (vmcnt(3) instead of (4))
+    __builtin_amdgcn_sched_barrier(0);
     load_codes(U, TB0, TB1);
     if constexpr (HP)
     {
@@ -1162,6 +1191,12 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         tl[5] = __builtin_amdgcn_s_memtime();
         tl[3] = ((uint64_t)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
                 (uint32_t)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_MISS)
+        tl[38] = missMask;
+        tl[39] = missCount;
+        tl[40] = spinCount;
+        tl[41] = spin0;
+#endif
     }
 }
 
@@ -1582,12 +1617,26 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_STRIPS)
     if (kBand && a.num_bands > 0 && !bandRole) return;  // timing ablation: the bands alone (results wrong)
 #endif
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_XCD)
+    bool xcdFirst = true;
+#endif
     while (true)
     {
         __syncthreads();  // every wave is done with the previous group's rings
         if (threadIdx.x == 0)
         {
             const bool aborted = __hip_atomic_load(&a.ctrl->abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_XCD)
+            // experiment: band groups placed statically so that consecutive groups share an XCD
+            // (workgroup b runs on XCD b % 8): groups x * per .. x * per + per - 1 on XCD x
+            if (bandRole && ngroups % 8 == 0 && a.band_wgs == ngroups)
+            {
+                const int per = ngroups / 8;
+                H.group = aborted || !xcdFirst ? ngroups : ((int)blockIdx.x % 8) * per + (int)blockIdx.x / 8;
+                xcdFirst = false;
+            }
+            else
+#endif
             H.group = aborted ? ngroups : (int)atomicAdd(qhead, 1u);
             H.nwaves = W;
         }

@@ -4,7 +4,7 @@
 set -e
 tag=$1; shift
 root=$(cd "$(dirname "$0")/.." && pwd)
-src=$root/sequence-alignment-gpu_amd/csrc
+src=${SRC_DIR:-$root/sequence-alignment-gpu_amd/csrc}  # SRC_DIR: build other sources (e.g. a git worktree's)
 out=/tmp/sa_build_exp/$tag
 mkdir -p "$out"
 # GEN_ENV="SA_GEN_BAND_PF_STEP=14 ..." regenerates the fill steps with those generator settings into a

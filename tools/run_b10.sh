@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 : > gpurun_out/b10.log
 for rep in 1 2; do
-  for lib in bst bs0 bs8 bp13 bp15; do
+  for lib in bst bx bs0 bs8 bp13 bp15; do
     for mode in 0 1; do
       echo "$lib mode=$mode " >> gpurun_out/b10.log
       SA_HIP_LIB=$PWD/build_exp/libsa_$lib.so timeout -k 10 120 python tools/band_stamps.py 32768 $mode 2>/dev/null | grep "^{" >> gpurun_out/b10.log || { echo failed $lib; exit 1; }
