@@ -399,17 +399,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     const int kb = a.key_bits;
     const int rowTop = sd.row0 + lane * R;
     int prof[R];
-    // row letters: unconditional loads (rows past m read row m's letter and drop it), all in flight
-    // together rather than one round trip each behind a branch (R up to 32)
-    int8_t lt[R];
-    sfor<R>([&](auto Rc) {
-        constexpr int rho = decltype(Rc)::value;
-        lt[rho] = a.pattern[pd.pattern_off + max(min(rowTop + rho, m), 1) - 1];
-    });
     sfor<R>([&](auto Rc) {
         constexpr int rho = decltype(Rc)::value;
         const int i = rowTop + rho;
-        int c = i <= m ? (int)lt[rho] : 0;
+        int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
         c = min(max(c, 0), a.A - 1);
         prof[rho] = SK == kProf ? a.prof_tab[c] : SK == kTable ? c * a.A : c;
     });
@@ -1245,20 +1238,11 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
     const int g = a.gap;
     const int rowTop = 1 + lane * R;
     uint32_t rsel[R];
-    // the 2R row letters: every load unconditional (rows past m read row m's letter and drop it), so
-    // the 2R loads are in flight together instead of one round trip each behind a branch
-    int8_t lA[R], lB[R];
-    sfor<R>([&](auto Rc) {
-        constexpr int rho = decltype(Rc)::value;
-        const int i = max(min(rowTop + rho, m), 1);
-        lA[rho] = a.pattern[pA.pattern_off + i - 1];
-        lB[rho] = a.pattern[pB.pattern_off + i - 1];
-    });
     sfor<R>([&](auto Rc) {
         constexpr int rho = decltype(Rc)::value;
         const int i = rowTop + rho;
-        const int cA = i <= m ? min(max((int)lA[rho], 0), a.A - 1) : 0;
-        const int cB = i <= m ? min(max((int)lB[rho], 0), a.A - 1) : 0;
+        const int cA = i <= m ? min(max((int)a.pattern[pA.pattern_off + i - 1], 0), a.A - 1) : 0;
+        const int cB = i <= m ? min(max((int)a.pattern[pB.pattern_off + i - 1], 0), a.A - 1) : 0;
         rsel[rho] = (uint32_t)cA | 0x0c00u | ((uint32_t)(4 + cB) << 16) | 0x0c000000u;
     });
     // column profiles {colA, colB} per column, in pair A's code block (2 dwords per column)

@@ -6,7 +6,7 @@ tail -n 2 gpurun_out/b12_tests.log
 : > gpurun_out/b12_ab.log
 for rep in 1 2 3; do
   for lib in new old; do
-    for w in headline local dna8k batch; do
+    for w in headline local dna8k; do
       if [ $lib = old ]; then export SA_HIP_LIB=$PWD/build_exp/libsa_old.so; else unset SA_HIP_LIB; fi
       timeout -k 10 200 python bench.py --workload $w --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/b12_x.json 2> gpurun_out/b12_x.err || { tail -n 20 gpurun_out/b12_x.err; exit 1; }
       echo "$rep $lib $w $(python tools/show_bench.py gpurun_out/b12_x.json)" >> gpurun_out/b12_ab.log
