@@ -561,32 +561,36 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
 #endif
             // the stager's windows for this strip: origin reqO, entry jc at window (d >> 4), pair d & 15
             const int d = reqO - jc;
-            const bool near = reqSeq > 0 && d >= 0 && d < 16 * (kStageWin - 8);
-            // local: the stager's done word first, then its windows speculatively, in one LDS round
-            // trip (the wave's LDS reads execute in issue order, so windows read after a done word that
-            // matches were complete: the stager writes them before the word); local traceback -2.7 %,
-            // global +2 % (profiles/r04/ab_walkspec_v1.log), so global reads the word, then the windows
-            uint32_t Ws[8];
-            int sdone = 0;
+            bool hit;
             if constexpr (LOCAL)
             {
-                sdone = ((volatile int *)req)[3];
+                // the stager's done word first, then its windows speculatively, in one LDS round trip
+                // (the wave's LDS reads execute in issue order, so windows read after a done word that
+                // matches were complete: the stager writes them before the word); local traceback
+                // -2.7 %, but global +2 % (profiles/r04/ab_walkspec_v1.log): global keeps two trips
+                const bool near = reqSeq > 0 && d >= 0 && d < 16 * (kStageWin - 8);
+                const int sdone = ((volatile int *)req)[3];
                 asm volatile("" ::: "memory");
                 const uint32_t *src = swin[reqSeq & 1] + (near ? d >> 4 : 0) * kWave + lane;
+                uint32_t Ws[8];
                 sfor<8>([&](auto Wc) { Ws[decltype(Wc)::value] = src[decltype(Wc)::value * kWave]; });
+                hit = near && uniform(sdone) == reqSeq;
+                if (hit) sfor<8>([&](auto Wc) { W[decltype(Wc)::value] = Ws[decltype(Wc)::value]; });
             }
-            else if (near)
+            else
             {
-                sdone = ((volatile int *)req)[3];
-                if (uniform(sdone) == reqSeq)
+                hit = reqSeq > 0 && d >= 0 && d < 16 * (kStageWin - 8) && uniform(((volatile int *)req)[3]) == reqSeq;
+                if (hit)
                 {
                     const uint32_t *src = swin[reqSeq & 1] + (d >> 4) * kWave + lane;
-                    sfor<8>([&](auto Wc) { Ws[decltype(Wc)::value] = src[decltype(Wc)::value * kWave]; });
+                    sfor<8>([&](auto Wc) {
+                        constexpr int w = decltype(Wc)::value;
+                        W[w] = src[w * kWave];
+                    });
                 }
             }
-            if (near && uniform(sdone) == reqSeq)
+            if (hit)
             {
-                sfor<8>([&](auto Wc) { W[decltype(Wc)::value] = Ws[decltype(Wc)::value]; });
                 jo = reqO - 16 * (d >> 4);
                 u0 = 2 * (d & 15);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
