@@ -966,8 +966,13 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_CODES_CONST)
         s0 &= 63;  // timing ablation: cache-resident text codes (results wrong)
 #endif
-        const i32x4u va = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[0], s0, 0);
-        const i32x4u vb = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[1], s0, 0);
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_CODES_POLICY)
+        constexpr int kCodePolicy = SA_EXP_CODES_POLICY;  // experiment: cache policy bits of the loads
+#else
+        constexpr int kCodePolicy = 0;
+#endif
+        const i32x4u va = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[0], s0, kCodePolicy);
+        const i32x4u vb = __builtin_amdgcn_raw_buffer_load_b128(crsrc, coff[1], s0, kCodePolicy);
         dA[0] = va.x;
         dA[1] = va.y;
         dA[2] = va.z;
@@ -1152,10 +1157,27 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     using P3 = std::integral_constant<int, 3>;
     const int nSteps = sd.nsteps;  // a multiple of 2U
     int s0 = 0;
+    // L1 touch distance of the text codes (bodies): 32768² global fill -2.5 %, local +4 % at 6 (4 and
+    // 8 are slower; same-box A/Bs, profiles/r04/band_touch_v1.log, band_touch_v2.log), so global only
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_TOUCH)
+    constexpr int kTouch = SA_EXP_BAND_TOUCH;
+#else
+    constexpr int kTouch = LOCAL ? 0 : 6;
+#endif
+    int touchA = 0, touchB = 0;
     // quads of bodies up to `end` (a multiple of 2U), then at most one pair (process_strip's phases)
-    auto phase = [&](auto full, int end) __attribute__((always_inline)) {
+    auto phase = [&](auto full, auto touch, int end) __attribute__((always_inline)) {
         for (; s0 + 2 * U < end; s0 += 4 * U)
         {
+            if constexpr (decltype(touch)::value)
+            {
+                // one dword per lane of both rows kTouch bodies ahead, so the code loads of that body
+                // find their lines in the CU's L1; consumed a quad later, so that no compiler wait
+                // stands on it (clamped to the furthest offset the code loads themselves reach)
+                asm volatile("" ::"v"(touchA), "v"(touchB));
+                touchA = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff[0], min(s0 + kTouch * U, nSteps + U), 0);
+                touchB = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff[1], min(s0 + kTouch * U, nSteps + U), 0);
+            }
             set_quad(s0);
             body(P0{}, full, s0, TA0, TA1, TC0, TC1);
             body(P1{}, full, s0 + U, TB0, TB1, TD0, TD1);
@@ -1178,8 +1200,19 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         }
     };
     // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered), then the rest
-    phase(std::true_type{}, min(nSteps, max(0, (n - U) / (2 * U) * (2 * U))));
-    phase(std::false_type{}, nSteps);
+    // the touch (DNA-sized alphabets only: protein 4096² measured 3 % slower with it) selects one of two
+    // copies of the loops, each with its own fixed wait counts
+    const int fullEnd = min(nSteps, max(0, (n - U) / (2 * U) * (2 * U)));
+    if (kTouch > 0 && a.A <= 4)
+    {
+        phase(std::true_type{}, std::integral_constant<bool, (kTouch > 0)>{}, fullEnd);
+        phase(std::false_type{}, std::integral_constant<bool, (kTouch > 0)>{}, nSteps);
+    }
+    else
+    {
+        phase(std::true_type{}, std::false_type{}, fullEnd);
+        phase(std::false_type{}, std::false_type{}, nSteps);
+    }
     if (a.timeline && lane == 0)
     {
         // band records follow the strips' (kTimelineWords words each)
