@@ -1158,7 +1158,9 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     const int nSteps = sd.nsteps;  // a multiple of 2U
     int s0 = 0;
     // L1 touch distance of the text codes (bodies): 32768² global fill -2.5 %, local +4 % at 6 (4 and
-    // 8 are slower; same-box A/Bs, profiles/r04/band_touch_v1.log, band_touch_v2.log), so global only
+    // 8 are slower; same-box A/Bs, profiles/r04/band_touch_v1.log, band_touch_v2.log), so global only.
+    // (Sensitive to code layout: gating it on the alphabet with a second copy of the loops lost the
+    // gain, profiles/r04/band_touch_v3.log; protein 4096² pays about 3 %.)
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_TOUCH)
     constexpr int kTouch = SA_EXP_BAND_TOUCH;
 #else
@@ -1200,19 +1202,8 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         }
     };
     // bodies whose next feed lies in columns 1..n (every feed lane needed and delivered), then the rest
-    // the touch (DNA-sized alphabets only: protein 4096² measured 3 % slower with it) selects one of two
-    // copies of the loops, each with its own fixed wait counts
-    const int fullEnd = min(nSteps, max(0, (n - U) / (2 * U) * (2 * U)));
-    if (kTouch > 0 && a.A <= 4)
-    {
-        phase(std::true_type{}, std::integral_constant<bool, (kTouch > 0)>{}, fullEnd);
-        phase(std::false_type{}, std::integral_constant<bool, (kTouch > 0)>{}, nSteps);
-    }
-    else
-    {
-        phase(std::true_type{}, std::false_type{}, fullEnd);
-        phase(std::false_type{}, std::false_type{}, nSteps);
-    }
+    phase(std::true_type{}, std::integral_constant<bool, (kTouch > 0)>{}, min(nSteps, max(0, (n - U) / (2 * U) * (2 * U))));
+    phase(std::false_type{}, std::integral_constant<bool, (kTouch > 0)>{}, nSteps);
     if (a.timeline && lane == 0)
     {
         // band records follow the strips' (kTimelineWords words each)
