@@ -1,0 +1,20 @@
+# round-4 check 23: band code touch distance for local (and global): none, 2, 3, 12 bodies ahead
+mkdir -p gpurun_out
+: > gpurun_out/b23.log
+for rep in 1 2 3; do
+  for lib in t0 t2 t3 t12; do
+    for mode in 1 0; do
+      echo "$lib mode=$mode " >> gpurun_out/b23.log
+      SA_HIP_LIB=$PWD/build_exp/libsa_$lib.so timeout -k 10 120 python tools/band_miss.py 32768 $mode 2>/dev/null | grep "^{" >> gpurun_out/b23.log || { echo failed $lib; exit 1; }
+    done
+  done
+done
+python3 - <<'PY'
+import ast
+cur=None
+for l in open('gpurun_out/b23.log'):
+    l=l.strip()
+    if not l.startswith('{'): cur=l; continue
+    d=ast.literal_eval(l)
+    if 'total_us' in d: print(f"{cur:12s} total {d['total_us']:7.1f} lag_in {d['lag_in_group_ns']:7.1f} cross {d['lag_cross_ns']:7.1f}")
+PY
