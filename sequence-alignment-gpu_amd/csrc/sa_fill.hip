@@ -934,7 +934,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 // the same inputs). Bands exist for every band of a pair but its last (whose bottom row feeds
 // nothing) and need no final state; the local recurrence saturates H = X - g at 0 with one clamped
 // subtract (g >= 0, X >= 0), so local is banded as well.
-template <bool LOCAL, bool HP, bool HN>
+template <bool LOCAL, bool HP, bool HN, bool TOUCH>
 __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = 16;
@@ -1158,13 +1158,13 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     const int nSteps = sd.nsteps;  // a multiple of 2U
     int s0 = 0;
     // L1 touch distance of the text codes (bodies): 32768² global fill -2.5 %, local +4 % at 6 (4 and
-    // 8 are slower; same-box A/Bs, profiles/r04/band_touch_v1.log, band_touch_v2.log), so global only.
-    // (Sensitive to code layout: gating it on the alphabet with a second copy of the loops lost the
-    // gain, profiles/r04/band_touch_v3.log; protein 4096² pays about 3 %.)
+    // 8 are slower; same-box A/Bs, profiles/r04/band_touch_v1.log, band_touch_v2.log), so global only,
+    // and DNA-sized alphabets only (protein 4096² pays about 4 %): a kernel of its own (TOUCH), since a
+    // second copy of the loops inside one kernel lost the gain (profiles/r04/band_touch_v3.log)
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_BAND_TOUCH)
     constexpr int kTouch = SA_EXP_BAND_TOUCH;
 #else
-    constexpr int kTouch = LOCAL ? 0 : 6;
+    constexpr int kTouch = TOUCH && !LOCAL ? 6 : 0;
 #endif
     int touchA = 0, touchB = 0;
     // quads of bodies up to `end` (a multiple of 2U), then at most one pair (process_strip's phases)
@@ -1616,7 +1616,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK, bool CHAIN>
+template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -1706,8 +1706,8 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
                         // -0.8 % fill for round 3's score waves, profiles/r03/dual_dev/prio_timeline.log)
                         __builtin_amdgcn_s_setprio(2);
                         // (every band publishes its bottom row: kHasNext)
-                        if (f & kHasPrev) process_band<LOCAL, true, true>(a, L, rings, idx, w, lane);
-                        else process_band<LOCAL, false, true>(a, L, rings, idx, w, lane);
+                        if (f & kHasPrev) process_band<LOCAL, true, true, TOUCH>(a, L, rings, idx, w, lane);
+                        else process_band<LOCAL, false, true, TOUCH>(a, L, rings, idx, w, lane);
                         __builtin_amdgcn_s_setprio(0);
                         continue;
                     }
@@ -1744,6 +1744,16 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
     if (chain)
     {
         const size_t lds = std::max(group_lds_bytes(W), (size_t)a.chain_lds);
+        if constexpr (R == 1 && SK == kArr8 && !LOCAL)
+            if (a.num_bands > 0 && a.A <= 4)
+            {
+                // global band fill of a DNA-sized alphabet: the kernel whose bands touch the codes ahead
+                if (lds > 65536)
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
+                return;
+            }
         if (lds > 65536)
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true>),
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
