@@ -193,8 +193,13 @@ class Chunked:
             row += j.plan.num_pairs
 
     def results(self) -> np.ndarray:
-        """Every pair's sa_result (numpy structured array; one copy per plan, no per-pair objects)."""
-        return np.concatenate([j.plan.results_array(self.s_fill.cuda_stream) for j in self.jobs])
+        """Every pair's sa_result (numpy structured array; one copy per plan, no per-pair objects).
+        Raises if the fill aborted or any pair's status is not SA_OK."""
+        res = np.concatenate([j.plan.results_array(self.s_fill.cuda_stream) for j in self.jobs])
+        if len(res) and res["status"].any():
+            bad = int(np.flatnonzero(res["status"])[0])
+            raise RuntimeError(f"pair {bad} has status {int(res['status'][bad])}")
+        return res
 
 
 def main_native(args) -> None:
@@ -446,7 +451,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if args.workload != "batch" else "strong",
             "vs_baseline": None,
-            "dtype": "int32",
+            # the pair-packed batch fill computes the int32 recurrence in u16 halves under a range guard
+            # (bit-exact on every pair: DESIGN.md §3.1b); every other fill computes in int32
+            "dtype": "u16x2 (int32 semantics)" if args.workload == "batch" and not os.environ.get("SA_NO_PAIR16")
+            else "int32",
             "data": DATA[args.workload],
             "config": dict(workload, rows_per_lane=info["rows_per_lane"], strips_per_gpu=info["num_strips"]),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -115,9 +115,12 @@ void free_cache_slot(ShardCache &c)
     c = ShardCache();
 }
 
+// atexit: a thread still inside sa_align_batch holds the lock and uses these objects, so the frees
+// are skipped then (leaking at exit is harmless; blocking here would deadlock the shutdown)
 void release_batch_cache()
 {
-    std::lock_guard<std::mutex> lock(g_batch_mu);
+    std::unique_lock<std::mutex> lock(g_batch_mu, std::try_to_lock);
+    if (!lock.owns_lock()) return;
     int cur = 0;
     (void)hipGetDevice(&cur);
     for (ShardCache &c : g_cache) free_cache_slot(c);

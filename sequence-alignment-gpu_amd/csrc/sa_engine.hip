@@ -1072,6 +1072,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     x.out_text = pl->d_out_text;
     x.out_pattern = pl->d_out_pattern;
     x.results = pl->d_results;
+    x.ctrl = pl->d_ctrl;
     x.A = pl->A;
     std::memcpy(x.alphabet, pl->alphabet, 33);
     // records per pair: one per row (row walk, R = 1) or per column (column walk)

@@ -1726,14 +1726,6 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
             }
         }
     }
-#if defined(SA_EXPERIMENT) && defined(SA_EXP_HOLD)
-    // experiment: finished workgroups stay resident (sleeping) until every workgroup has finished
-    if (threadIdx.x == 0)
-        while (__hip_atomic_load(&a.ctrl->queue_head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-               (unsigned)(a.num_groups + gridDim.x))
-            __builtin_amdgcn_s_sleep(127);
-    __syncthreads();
-#endif
 }
 
 // Fill launches, one translation unit per strip height R (fill_r<R>.hip instantiates

@@ -52,6 +52,7 @@ struct ExpandArgs {
     const TbHead *heads;
     char *out_text, *out_pattern;
     sa_result *results;
+    const Control *ctrl;  // the plan's control word: a fill abort or bad input becomes every pair's status
     int32_t A;
     int32_t chunk_recs;  // records per expansion block (launch_expand sets it)
     char alphabet[33];

@@ -52,7 +52,7 @@ def gather_device(buf, num_pairs: int, world: int, rank: int):
     """Gathers every rank's sa_result rows, already in a (width, 4) int64 tensor on the rank's device
     (Plan.copy_results: bit copies of sa_result, so column 0 is score | status << 32), to rank 0 with
     one collective and no host round trip before it; rank 0 brings the gathered block to the host in
-    one copy. Returns the (num_pairs, 4) int64 FIELDS array in global pair order on rank 0, None
+    one copy and raises RuntimeError if any pair's status is not SA_OK. Returns the (num_pairs, 4) int64 FIELDS array in global pair order on rank 0, None
     elsewhere (as gather_array)."""
     import numpy as np
     import torch
@@ -67,6 +67,14 @@ def gather_device(buf, num_pairs: int, world: int, rank: int):
     for r in range(world):
         idx = shard(num_pairs, world, r)
         rows = allp[r, : len(idx)]
+        # sa_result.status (bits 32..63 of word 0): the expand kernel writes the fill's abort / bad-input
+        # state into every pair, so a failed pair on any rank fails the gather here instead of reaching
+        # rank 0 as a score
+        status = (rows[:, 0] >> 32) & 0xFFFFFFFF
+        if status.any():
+            bad = int(np.flatnonzero(status)[0])
+            raise RuntimeError(f"gather_device: rank {r} pair {idx[bad]} has status {int(status[bad])} "
+                               f"({int(np.count_nonzero(status))} of {len(idx)} pairs of that rank failed)")
         score = rows[:, 0] & 0xFFFFFFFF
         out[idx, 0] = np.where(score >= 1 << 31, score - (1 << 32), score)
         out[idx, 1:] = rows[:, 1:]

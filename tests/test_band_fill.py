@@ -5,7 +5,7 @@ its knobs once per process) with SA_BAND=1 / 0 on small chains, cell by cell aga
 DIRECTION matrix (alignSequenceCPU.cpp:116-201 local, :203-284 global) and the full alignment
 (:10-114), for both modes and gaps 5 / 0 (and -2, global only: local kArr8 needs g >= 0, the plan
 falls back to the one-wave fill there); at the default shapes (>= 16384 columns, several band and
-strip groups); with several chained pairs per plan (band groups spanning pairs); and a local then a
+strip groups); a 23-letter BLOSUM50 pair in both modes (the global band kernel without the code touch); with several chained pairs per plan (band groups spanning pairs); and a local then a
 global 32768^2 call in one fresh process, against the reference's recorded outputs (large.json)."""
 from __future__ import annotations
 
@@ -26,9 +26,10 @@ from sa_amd import engine, synthetic
 from sa_amd.batch import DeviceBatch
 S = synthetic.blast_matrix()
 bad = []
-def check(mode, n, m, gap, seed, related):
-    t = synthetic.random_sequence(seed, n, 4)
-    p = synthetic.mutate(t, seed + 1, 4, m) if related else synthetic.random_sequence(seed + 2, m, 4)
+def check(mode, n, m, gap, seed, related, S=S):
+    A = S.shape[0]
+    t = synthetic.random_sequence(seed, n, A)
+    p = synthetic.mutate(t, seed + 1, A, m) if related else synthetic.random_sequence(seed + 2, m, A)
     b = DeviceBatch(mode, S, gap, [t], [p], rows_per_lane=1)
     b.fill()
     got = b.directions(0)
@@ -49,6 +50,11 @@ cases = [(3000, 2900, 5), (2100, 1000, 0), (700, 1100, 3), (4500, 260, -2), (150
 for k, (n, m, gap) in enumerate(cases):
     for mode in (0, 1):
         check(mode, n, m, gap, 800 + 10 * k, k % 2 == 0)
+# protein (23 letters, BLOSUM50): the global band kernel without the code touch (the touching kernel
+# serves alphabets of at most 4 letters) and the local band kernel, cell by cell
+B50 = np.array(json.load(open(sys.argv[1] + "/tests/golden/matrices.json"))["blosum50"], np.int32).reshape(23, 23)
+for mode in (0, 1):
+    check(mode, 3000, 1100, 5, 900 + mode, mode == 0, S=B50)
 # several chained pairs in one plan, even strip counts (each pair's first strip even): band groups
 # and strip groups span pair boundaries
 ts = [synthetic.random_sequence(1000 + k, 1800 + 97 * k, 4) for k in range(5)]

@@ -126,7 +126,7 @@ def test_gather_array_world2():
     assert np.uint64(got[0, 2].view(np.uint64)) == np.uint64((1 << 64) - 1)
 
 
-def _device_worker(rank, world, port, num, q):
+def _device_worker(rank, world, port, num, q, bad_pair=-1):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "sequence-alignment-gpu_amd", "python"))
     import numpy as np
@@ -140,14 +140,17 @@ def _device_worker(rank, world, port, num, q):
     mine = distributed.shard(num, world, rank)
     arr = np.zeros(len(mine), RESULT_DTYPE)
     arr["score"] = [10 * i - 7 for i in mine]
-    arr["status"] = [i % 2 for i in mine]  # the word beside the score must not leak into it
+    arr["status"] = [5 if i == bad_pair else 0 for i in mine]  # SA_ERR_TIMEOUT on the injected pair
     arr["num_bytes"] = [i + 3 for i in mine]
     arr["start_text"] = [(1 << 64) - 1 if i % 3 == 0 else i for i in mine]
     arr["start_pattern"] = [i * 5 for i in mine]
     # what Plan.copy_results leaves in the bench's gather buffer: raw sa_result bytes, (width, 4) int64
     buf = torch.full(((num + world - 1) // world, 4), -1, dtype=torch.int64)
     buf[: len(mine)] = torch.from_numpy(arr.view(np.int64).reshape(len(mine), 4).copy())
-    out = distributed.gather_device(buf, num, world, rank)
+    try:
+        out = distributed.gather_device(buf, num, world, rank)
+    except RuntimeError as e:
+        out = f"raised: {e}"
     if rank == 0:
         q.put(out)
     dist.destroy_process_group()
@@ -171,6 +174,24 @@ def test_gather_device_world2():
     for i in range(num):
         st = -1 if i % 3 == 0 else i
         assert got[i].tolist() == [10 * i - 7, i + 3, st, i * 5], i
+
+
+def test_gather_device_status_fails_loudly():
+    """A pair whose sa_result.status is not SA_OK on rank 1 (here SA_ERR_TIMEOUT, what the expand kernel
+    writes after a hand-off timeout) makes rank 0's gather raise instead of returning its score."""
+    num = 11
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_device_worker, args=(r, 2, port, num, q, 7)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert isinstance(got, str) and got.startswith("raised:"), got
+    assert "rank 1 pair 7 has status 5" in got, got
 
 
 def test_bench_launches_ranks_dry_run():

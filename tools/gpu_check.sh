@@ -20,4 +20,4 @@ for w in ${WORKLOADS:-headline local dna8k protein4k batch}; do
     { tail -n 20 gpurun_out/${tag}_$w.err; exit 1; }
   python tools/show_bench.py gpurun_out/${tag}_$w.json
 done
-bash tools/timeline.sh -m "32768 64 256"
+[ -n "$NO_TIMELINE" ] || bash tools/timeline.sh -m "32768 64 256"
