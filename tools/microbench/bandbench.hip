@@ -1,6 +1,6 @@
 // Lone-wave clocks per step of the score-chain recurrence with R rows per lane (development tool).
 // Steps come from tools/microbench/gen_bandbench.py (bandbench.inc). One wave per SIMD, 256
-// workgroups of 4 waves.
+// workgroups of 4 waves; then two waves per SIMD (8 waves per workgroup).
 //   python3 tools/microbench/gen_bandbench.py && hipcc -O3 --offload-arch=gfx950 \
 //       tools/microbench/bandbench.hip -o tools/microbench/bandbench
 #include <hip/hip_runtime.h>
@@ -10,7 +10,7 @@
 #include "bandbench.inc"
 
 #define KERNEL(NAME)                                                                          \
-    __global__ __launch_bounds__(256) void k_##NAME(int iters, long long *out, int *sink, int g) \
+    __global__ __launch_bounds__(512) void k_##NAME(int iters, long long *out, int *sink, int g) \
     {                                                                                         \
         const int lane = threadIdx.x & 63;                                                    \
         int r[NAME##_nregs];                                                                  \
@@ -22,18 +22,19 @@
         int s = 0;                                                                            \
         for (int i = 0; i < NAME##_nregs; ++i) s += r[i];                                     \
         sink[blockIdx.x * blockDim.x + threadIdx.x] = s;                                      \
-        if (lane == 0) out[blockIdx.x * 4 + threadIdx.x / 64] = (long long)(t1 - t0);        \
+        if (lane == 0) out[blockIdx.x * 8 + threadIdx.x / 64] = (long long)(t1 - t0);        \
     }                                                                                         \
-    void run_##NAME(long long *out, int *sink)                                                \
+    void run_##NAME(long long *out, int *sink, int wpg)                                       \
     {                                                                                         \
         const int iters = 2048, grid = 256;                                                   \
-        for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(k_##NAME, dim3(grid), dim3(256), 0, 0, iters, out, sink, 5); \
+        for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(k_##NAME, dim3(grid), dim3(64 * wpg), 0, 0, iters, out, sink, 5); \
         (void)hipDeviceSynchronize();                                                         \
-        static long long h[256 * 4];                                                          \
+        static long long h[256 * 8];                                                          \
         (void)hipMemcpy(h, out, sizeof(h), hipMemcpyDeviceToHost);                            \
         double s = 0;                                                                         \
-        for (int i = 0; i < grid * 4; ++i) s += (double)h[i] / ((double)iters * NAME##_steps); \
-        printf("{\"stream\": \"%s\", \"steps_per_block\": %d, \"clk_per_step\": %.2f}\n", #NAME, NAME##_steps, s / (grid * 4)); \
+        for (int b = 0; b < grid; ++b)                                                        \
+            for (int w = 0; w < wpg; ++w) s += (double)h[b * 8 + w] / ((double)iters * NAME##_steps); \
+        printf("{\"stream\": \"%s\", \"waves_per_simd\": %d, \"steps_per_block\": %d, \"clk_per_step\": %.2f}\n", #NAME, wpg / 4, NAME##_steps, s / (grid * wpg)); \
     }
 
 KERNEL(band_r1g)
@@ -49,15 +50,16 @@ int main()
 {
     long long *out;
     int *sink;
-    (void)hipMalloc(&out, sizeof(long long) * 256 * 4);
-    (void)hipMalloc(&sink, 256 * 256 * 4);
-    run_band_r1g(out, sink);
-    run_band_r1l(out, sink);
-    run_band_r2g(out, sink);
-    run_band_r2l(out, sink);
-    run_band_r3g(out, sink);
-    run_band_r3l(out, sink);
-    run_band_r4g(out, sink);
-    run_band_r4l(out, sink);
+    (void)hipMalloc(&out, sizeof(long long) * 256 * 8);
+    (void)hipMalloc(&sink, 256 * 512 * 4);
+    for (int wpg = 4; wpg <= 8; wpg += 4)
+    {
+        run_band_r1g(out, sink, wpg);
+        run_band_r1l(out, sink, wpg);
+        run_band_r2g(out, sink, wpg);
+        run_band_r2l(out, sink, wpg);
+        run_band_r3g(out, sink, wpg);
+        run_band_r4g(out, sink, wpg);
+    }
     return 0;
 }
