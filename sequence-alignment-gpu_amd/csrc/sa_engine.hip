@@ -192,8 +192,9 @@ struct Knobs {
     int waves_per_group = 0;        // SA_WAVES_PER_GROUP: force W (1..4)
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
     int band = -1;                  // SA_BAND: 1 / 0 force the band fill (128-row score strips
-                                    // feeding the 64-row strips, sa_fill.hip process_band) on / off;
-                                    // default: on wherever it applies (plan_create)
+                                    // feeding the 64-row strips, sa_fill.hip process_band) on / off
+                                    // (1 also past kBandPersistRows); default: on wherever it applies
+                                    // (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
@@ -201,6 +202,7 @@ struct Knobs {
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
     bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
+    int max_cus = 0;                // SA_MAX_CUS: plan as if the device had at most this many CUs (tests)
 };
 
 const Knobs &knobs()
@@ -220,6 +222,7 @@ const Knobs &knobs()
         v.tb_timing = get("SA_TB_TIMING");
         v.tb_generic = get("SA_TB_GENERIC") != nullptr;
         if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
+        if (const char *e = get("SA_MAX_CUS")) v.max_cus = std::max(0, std::atoi(e));
         return v;
     }();
     return k;
@@ -343,6 +346,8 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
 
 // Waves per workgroup (strips per group). Chains of strips (pairs taller than one strip) hand
 // their rows off through LDS inside a group; single-strip pairs gain nothing from grouping.
+constexpr int64_t kBandPersistRows = 131072;  // band fill with persistent workers up to this many rows
+
 int choose_W(const std::vector<PairDesc> &pairs)
 {
     const int w = knobs().waves_per_group;
@@ -669,6 +674,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
     auto restore = [&]() { (void)hipSetDevice(cur); };
     if (hipSetDevice(device) != hipSuccess) { delete pl; restore(); return fail(SA_ERR_HIP, "hipSetDevice failed"); }
     pl->num_cu = device_cus(device);
+    if (knobs().max_cus > 0) pl->num_cu = std::min(pl->num_cu, knobs().max_cus);
 
     // ---- layout ----
     const int R = pl->R, U = pl->U, RB = kWave * R;
@@ -752,7 +758,13 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         for (const PairDesc &d : pl->pairs) nb += std::max(0, (d.num_strips + 1) / 2 - 1);
         const int64_t stripGroups = ((int64_t)pl->strips.size() + pl->W - 1) / pl->W;
         const int64_t bandGroups = (nb + pl->W - 1) / pl->W;
-        band = band && nb > 0 && stripGroups + bandGroups <= pl->num_cu;
+        // every group in flight at once, or (persistent band and strip workgroups, FillArgs::band_wgs)
+        // chains up to kBandPersistRows rows: past them the fill is throughput-bound and the bands' work
+        // on top of the strips' costs more than their shorter ramp saves
+        int64_t mmax = 0;
+        for (const PairDesc &d : pl->pairs) mmax = std::max<int64_t>(mmax, (int64_t)d.pattern_len);
+        band = band && nb > 0 &&
+               (stripGroups + bandGroups <= pl->num_cu || ((mmax <= kBandPersistRows || knobs().band == 1) && pl->num_cu >= 4));
         if (band)
         {
             // bands b = 0 .. B-2 of each pair (B = ceil(strips / 2); the last band's bottom row feeds
@@ -1008,6 +1020,15 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             a.band_wgs = a.num_band_groups;
             a.chain_lds = std::max(a.chain_lds, 96 * 1024);
             grid = a.num_band_groups + a.num_groups;
+            if (grid > pl->num_cu)
+            {
+                // more groups than CUs: persistent workers, each taking groups from its queue in chain
+                // order until it is empty (a group waits only for groups dequeued before it, so every
+                // worker count makes progress); the split that a model of the band and strip chains
+                //  puts ahead for 65536^2 .. 120000^2 is about 0.31 of the CUs to bands
+                a.band_wgs = std::max(1, std::min(a.num_band_groups, (int)(0.31 * pl->num_cu + 0.5)));
+                grid = a.band_wgs + std::max(1, std::min(a.num_groups, pl->num_cu - a.band_wgs));
+            }
         }
         launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
         HIP_TRY(hipGetLastError());

@@ -5,7 +5,8 @@ its knobs once per process) with SA_BAND=1 / 0 on small chains, cell by cell aga
 DIRECTION matrix (alignSequenceCPU.cpp:116-201 local, :203-284 global) and the full alignment
 (:10-114), for both modes and gaps 5 / 0 (and -2, global only: local kArr8 needs g >= 0, the plan
 falls back to the one-wave fill there); at the default shapes (>= 16384 columns, several band and
-strip groups); a 23-letter BLOSUM50 pair in both modes (the global band kernel without the code touch); with several chained pairs per plan (band groups spanning pairs); and a local then a
+strip groups); more groups than CUs (SA_MAX_CUS: persistent band and strip workers); a 23-letter
+BLOSUM50 pair in both modes (the global band kernel without the code touch); with several chained pairs per plan (band groups spanning pairs); and a local then a
 global 32768^2 call in one fresh process, against the reference's recorded outputs (large.json)."""
 from __future__ import annotations
 
@@ -74,6 +75,13 @@ for mode, gap in ((0, 5), (0, -2), (1, 5), (1, 0)):
 print("BAND_OK" if not bad else "BAND_BAD %r" % (bad,))
 '''
 
+# more band and strip groups than the (capped) CUs: persistent workers loop over their queues
+PERSIST = HEAD + r'''
+for mode, gap in ((0, 5), (1, 5)):
+    check(mode, 2048, 8192, gap, 5000 + mode, False)
+print("BAND_OK" if not bad else "BAND_BAD %r" % (bad,))
+'''
+
 LARGE = r'''
 import sys, json
 sys.path[:0] = [sys.argv[1] + "/sequence-alignment-gpu_amd/python", sys.argv[1] + "/tests"]
@@ -111,6 +119,14 @@ def test_band_fill_vs_oracle(band):
 @pytest.mark.gpu
 def test_band_fill_default_shapes_vs_oracle():
     _run(DEFAULT)
+
+
+@pytest.mark.gpu
+def test_band_fill_persistent_workers_vs_oracle():
+    """SA_MAX_CUS=16 plans a 2048 x 8192 pair (16 band groups + 32 strip groups) on 16 CUs: 5 band and
+    11 strip workgroups take their groups from the queues in chain order; every cell of the direction
+    matrix and the alignment must still be the reference's (both modes)."""
+    _run(PERSIST, SA_MAX_CUS="16")
 
 
 @pytest.mark.gpu
