@@ -162,7 +162,10 @@ int sa_plan_info(const sa_plan *plan, int64_t *num_strips, int32_t *rows_per_lan
 /* Verification: synchronise `stream` and decode pair `index`'s direction bit-planes into the
  * reference's (pattern_len+1) x (text_len+1) byte DIRECTION matrix (LEFT=0, DIAG=1, TOP=2, STOP=3;
  * row 0 / column 0 as the reference fill sets them, alignSequenceCPU.cpp:145-164, :232-248), so the
- * fill can be compared byte-for-byte with the reference's M. M_out must hold (m+1)*(n+1) bytes. */
+ * fill can be compared byte-for-byte with the reference's M. Local plans with one row per lane
+ * (rows_per_lane 1) hold no STOP bit: their interior cells decode to the reference's decision before
+ * its STOP override (alignSequenceCPU.cpp:181-189; the reference's STOP cells are those whose score
+ * is 0, which the traceback recomputes). M_out must hold (m+1)*(n+1) bytes. */
 int sa_plan_fetch_directions(sa_plan *plan, int64_t index, uint8_t *M_out, void *stream);
 
 /* Device pointer to the per-pair sa_result array written by sa_plan_traceback. */

@@ -79,7 +79,8 @@ def align(mode: int, text: np.ndarray, pattern: np.ndarray, S: np.ndarray, gap: 
 
 def fill_only(mode: int, text: np.ndarray, pattern: np.ndarray, S: np.ndarray, gap: int,
               M: np.ndarray | None = None) -> int:
-    """Fill the (m+1)x(n+1) direction matrix only (tests/benchmarks.cu:153-154 convention)."""
+    """Fill the (m+1)x(n+1) direction matrix only (tests/benchmarks.cu:153-154 convention). mode 2: local
+    with the raw decision of every interior cell (no STOP override; the engine's rows_per_lane 1 planes)."""
     text = np.ascontiguousarray(text, dtype=np.int8)
     pattern = np.ascontiguousarray(pattern, dtype=np.int8)
     S = np.ascontiguousarray(S, dtype=np.int32)

@@ -11,7 +11,9 @@ static inline int32_t imax(int32_t a, int32_t b) { return a > b ? a : b; }
 
 /* One DP sweep for both modes. Two rolling int32 rows, as the reference keeps
  * (alignSequenceCPU.cpp:133-134 / :220-221); the direction of every cell goes to M. */
-static int32_t sweep(int local, const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
+/* raw (local): interior cells keep the decision before the STOP override of :189 (the engine's R = 1
+ * direction planes hold exactly that; its STOP cells are the H == 0 ones). */
+static int32_t sweep(int local, int raw, const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
                      const int32_t *S, int32_t A, int32_t gap, uint8_t *M, uint64_t *maxIJ)
 {
     const uint64_t cols = n + 1, rows = m + 1;
@@ -50,7 +52,7 @@ static int32_t sweep(int local, const int8_t *text, uint64_t n, const int8_t *pa
             if (local)
             {
                 /* Non-positive best -> STOP and score 0 (:189-190); first strict max wins (:191-192). */
-                if (h <= 0) dir = ORACLE_STOP;
+                if (h <= 0 && !raw) dir = ORACLE_STOP;
                 cur[j] = h > 0 ? h : 0;
                 if (cur[j] > best) { best = cur[j]; bestIdx = i * cols + j; }
             }
@@ -71,20 +73,21 @@ static int32_t sweep(int local, const int8_t *text, uint64_t n, const int8_t *pa
 int32_t oracle_fill_nw(const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
                        const int32_t *S, int32_t A, int32_t gap, uint8_t *M)
 {
-    return sweep(0, text, n, pattern, m, S, A, gap, M, NULL);
+    return sweep(0, 0, text, n, pattern, m, S, A, gap, M, NULL);
 }
 
 int32_t oracle_fill_sw(const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
                        const int32_t *S, int32_t A, int32_t gap, uint8_t *M, uint64_t *maxIJ)
 {
-    return sweep(1, text, n, pattern, m, S, A, gap, M, maxIJ);
+    return sweep(1, 0, text, n, pattern, m, S, A, gap, M, maxIJ);
 }
 
 int32_t oracle_fill_only(int mode, const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
                          const int32_t *S, int32_t A, int32_t gap, uint8_t *M)
 {
     uint64_t idx = 0;
-    return sweep(mode == 1, text, n, pattern, m, S, A, gap, M, &idx);
+    /* mode 2: local with raw decisions (see sweep) */
+    return sweep(mode >= 1, mode == 2, text, n, pattern, m, S, A, gap, M, &idx);
 }
 
 static void reverse_bytes(char *p, uint64_t len)

@@ -35,7 +35,9 @@ int oracle_align(int mode, const int8_t *text, uint64_t n, const int8_t *pattern
                  int32_t *score, uint64_t *num_bytes, uint64_t *start_text, uint64_t *start_pattern,
                  char *aligned_text, char *aligned_pattern);
 
-/* Fill only, timed by the caller (bench cpu_baseline, tests/benchmarks.cu:153-154 convention). */
+/* Fill only, timed by the caller (bench cpu_baseline, tests/benchmarks.cu:153-154 convention).
+ * mode 2: local with the raw decision of every interior cell (no STOP override, :189), as the
+ * engine's rows_per_lane 1 planes hold it. */
 int32_t oracle_fill_only(int mode, const int8_t *text, uint64_t n, const int8_t *pattern, uint64_t m,
                          const int32_t *S, int32_t A, int32_t gap, uint8_t *M);
 

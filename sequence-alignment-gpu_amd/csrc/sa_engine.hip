@@ -1081,6 +1081,10 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     w.key_rowbits = pl->key_rowbits;
     w.fast = kn.tb_generic ? 0 : 1;
     w.stager = kn.tb_stager ? 1 : 0;
+    w.text = pl->d_text_in;
+    w.pattern = pl->d_pattern_in;
+    w.score_tab = pl->d_table;
+    w.A = pl->A;
     launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "walk kernel")) return rc;
@@ -1219,7 +1223,9 @@ int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *strea
                 b1 = (w[NW + (e % CS) / 32] >> (31 - e % 32)) & 1u;
             }
             // global: plane1 is the raw "up > left" bit and DIAG wins (see run_body)
-            M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
+            // global, and local R = 1 (raw decisions, no STOP: sa_layout.h): DIAG wins over the raw
+            // "up > left"; local R > 1: the plane pair is the reference's code itself
+            M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL || R == 1 ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
         }
     }
     return SA_OK;

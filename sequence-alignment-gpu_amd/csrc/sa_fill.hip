@@ -201,7 +201,8 @@ enum BodyKind { kSteady = 0, kStart = 1, kGeneric = 2 };
 //   local, H with the gap folded into the score: X = max(Hdiag + S + g, max(Hleft, Hup), g),
 //     H = X - g (= max(X' - g, 0) for g > 0, X' - g for g <= 0: X' >= 0); DIAG iff Hdiag + S + g > max(Hleft,
 //     Hup) (the reference's D > max(L, U) with every candidate shifted by +g); raw TOP iff Hup >
-//     Hleft; STOP iff H == 0 (alignSequenceCPU.cpp:175-190).
+//     Hleft; STOP iff H == 0 (alignSequenceCPU.cpp:175-190), stored only for R > 1 (R = 1: the row
+//     walk recomputes H along the path, sa_walk.hip).
 // Lane moves per step: `up` (the row above each lane's first row) is F[R-1] of lane k-1 by a DPP
 // wave_shr:1 whose `old` operand is this step's feed register Q (lane 0 keeps Q's lane 0 = the
 // strip above's bottom value for this column); Q is dead afterwards, so the DPP writes in place. The
@@ -256,9 +257,10 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 acc[0][w] = push_sign(acc[0][w], M - D);      // DIAG
                 acc[1][w] = push_sign(acc[1][w], left - up);  // raw "up > left" (global) / raw TOP (local)
             }
-            else if constexpr (!LOCAL)
+            else
             {
-                // R = 1: interleaved word, DIAG then raw "up > left" per slot (sa_layout.h)
+                // R = 1: interleaved word, DIAG then raw "up > left" (local: raw TOP) per slot (sa_layout.h);
+                // local STOP (H == 0) is not stored: the row walk recomputes H along the path
                 acc[0][0] = push_sign(push_sign(acc[0][0], M - D), left - up);
             }
             int Fn;
@@ -272,12 +274,6 @@ __device__ __forceinline__ void run_body(const int *__restrict__ ldsS, int s0, i
                 const int X = max(max(D, M), g);
                 Fn = X - g;
                 if constexpr (R > 1) acc[2][w] = push_sign(acc[2][w], Fn - 1);  // STOP (H == 0)
-                else
-                {
-                    // interleaved: DIAG|STOP, then (TOP & ~DIAG)|STOP (sign bits: Fn - 1 < 0 iff H == 0)
-                    const int dd = M - D;
-                    acc[0][0] = push_sign(push_sign(acc[0][0], dd | (Fn - 1)), ((left - up) & ~dd) | (Fn - 1));
-                }
                 const int key = (Fn << kb) + Ks;
                 if constexpr (RAMP) best[rho] = act ? max(best[rho], key) : best[rho];
                 else best[rho] = max(best[rho], key);
@@ -334,9 +330,8 @@ __device__ __forceinline__ void store_chunk(uint32_t *dst, const uint32_t (&acc)
 // of U = 16 steps every value is back in its field (F2 is a spare).
 struct StepRegs {
     int Q, Qn, diag, F;
-    int X[8], Y[8], Z[8];  // the plane word's direction differences, one byte per step (DIAG, TOP, STOP)
+    int X[8], Y[8];        // the plane word's direction differences, one byte per step (DIAG, TOP)
     int mk[8];             // mk[s] = 0x80808080 >> s (merge_asm)
-    int mz[4];             // mz[t] = 0xc0c0c0c0 >> 2t (local STOP bytes to both bits)
     uint32_t acc0, acc1;   // the chunk's two interleaved words (merge_asm)
     int bm;      // local: running max of (H << kb) - q over the body
     int T[4];    // text-profile words of the body (4 steps each)
@@ -633,19 +628,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     // the asm bodies' direction-difference bytes (kept across the two bodies of a plane word) and the
     // merge masks 0x80808080 >> g (opaque: built once per strip, not rematerialized per word)
-    int dX[8], dY[8], dZ[8], mkv[8], mzv[4];
+    int dX[8], dY[8], mkv[8];
     sfor<8>([&](auto Gc) {
         constexpr int g = decltype(Gc)::value;
-        dX[g] = dY[g] = dZ[g] = 0;
+        dX[g] = dY[g] = 0;
         int m;
         asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "i"((int)(0x80808080u >> g)));
         mkv[g] = m;
-    });
-    sfor<4>([&](auto Tc) {
-        constexpr int t = decltype(Tc)::value;
-        int m = 0;
-        if constexpr (LOCAL) asm volatile("v_mov_b32 %0, %1" : "=v"(m) : "i"((int)(0xc0c0c0c0u >> (2 * t))));
-        mzv[t] = m;
     });
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     // the compiler's vector-memory wait before each steady body is the most conservative over the
@@ -703,7 +692,6 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
                 constexpr int g = decltype(Gc)::value;
                 r.X[g] = dX[g];
                 r.Y[g] = dY[g];
-                if constexpr (LOCAL) r.Z[g] = dZ[g];
             });
             r.bm = -16;  // below every (H << kb) - q
             sfor<4>([&](auto Wc) { r.T[decltype(Wc)::value] = T[decltype(Wc)::value]; });
@@ -733,13 +721,11 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
                 constexpr int g = decltype(Gc)::value;
                 dX[g] = r.X[g];
                 dY[g] = r.Y[g];
-                if constexpr (LOCAL) dZ[g] = r.Z[g];
             });
             if constexpr ((POS & 1) == 1)
             {
                 // the chunk's second body: its bits into the two interleaved words for the store below
                 sfor<8>([&](auto Gc) { r.mk[decltype(Gc)::value] = mkv[decltype(Gc)::value]; });
-                if constexpr (LOCAL) sfor<4>([&](auto Tc) { r.mz[decltype(Tc)::value] = mzv[decltype(Tc)::value]; });
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_NO_MERGE)
                 // timing ablation: the chunk's words are two raw difference registers (results wrong)
                 acc[1][0] = (uint32_t)r.X[0] ^ (uint32_t)r.X[5];

@@ -19,7 +19,9 @@
 // row windows (two bits per cell) are funnel shifts of the lane's stream. The reference DIRECTION code (LEFT=0,
 // DIAG=1, TOP=2, STOP=3; SequenceAlignment.hpp:122) is
 //   global: plane0 = DIAG, plane1 = "up > left";  code = plane0 ? DIAG : plane1 ? TOP : LEFT
-//   local:  plane0 = DIAG|STOP, plane1 = (TOP&~DIAG)|STOP;  code = plane0 | plane1 << 1
+//   local, R = 1: as global (the raw decision of every cell); STOP is the cell's H == 0, which the
+//           row walk recomputes along the path (sa_walk.hip local_check), so no plane holds it
+//   local, R > 1: plane0 = DIAG|STOP, plane1 = (TOP&~DIAG)|STOP;  code = plane0 | plane1 << 1
 // That is 2 bits per cell written to HBM (the reference writes 1 byte per cell,
 // alignSequenceGPU.cu:142); the algorithmic figure used for the roofline stays 1 B/cell.
 //

@@ -43,6 +43,10 @@ struct WalkArgs {
     int32_t gap, key_rowbits;
     int32_t fast;                // 1: unrolled asm strip walk (0: the generic loop only; tests)
     int32_t stager;              // 1: row walk with the stager wave (0: the walker stages every strip)
+    // local row walk (R = 1 planes hold no STOP): H is recomputed along the path (local_check)
+    const int8_t *text, *pattern;  // the fill's inputs (alphabet indices)
+    const int32_t *score_tab;      // A x A, S + g (the plan's local table)
+    int32_t A;
 };
 
 struct ExpandArgs {

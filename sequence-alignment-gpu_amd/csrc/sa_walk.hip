@@ -499,15 +499,147 @@ __device__ void rw_stager(const WalkArgs &a, const uint32_t *mb, int64_t sstride
     }
 }
 
+// Local row walk: the stager also runs local_check on every strip the walker posts. The walk runs on
+// the global encoding (the R = 1 planes hold no STOP), so where traceBackSW ends -- the first cell
+// whose H is 0 (a STOP, alignSequenceCPU.cpp:18, :189) or the first move onto row 0 / column 0
+// (:44-46) -- comes from H followed along the path: a row entered at H_e adds g per LEFT cell
+// (H(left) = H + g, :176, :185-186), its leaving TOP adds g, its leaving DIAG subtracts S of its cell
+// (:178). Per strip (lane l = row 64 b + l + 1, walked from lane k down): the entry columns from a
+// prefix sum of the moves, the leaving DIAG cells' letters gathered from the inputs (in flight while
+// window requests are served), then a prefix sum of the H steps and one ballot for the first row
+// where the walk ends. The walker learns the verdict a strip or two later; the records it wrote past
+// it lie past nrec.
+__device__ void rw_stager_local(const WalkArgs &a, const PairDesc &sp, const uint32_t *mb, int64_t sstride, volatile int *req,
+                                uint32_t (*swin)[kStageWin * kWave], const int *stab, int (*chkBuf)[72], int *chkCtl, int lane)
+{
+    volatile int *ctl = (volatile int *)chkCtl;
+    const int64_t toff = (int64_t)uniform64(sp.text_off), poff = (int64_t)uniform64(sp.pattern_off);
+    int seen = 0, cseen = 0;
+    bool inflight = false, ended = false;
+    int Hc = 0;
+    int cb = 0, ck = 0, cn0 = 0;                              // the check in flight: strip, first lane, nrec before
+    int run = 0, dg = 0, ce = 0, lv = 0, pl = 0, tl = 0;      // per lane (row)
+    for (uint32_t spin = 1;; ++spin)
+    {
+        const int q = uniform(req[0]);
+        if (q < 0) return;
+        if (q != seen)
+        {
+            // window requests first: the walker is waiting for them
+            seen = q;
+            spin = 0;
+            const int b = uniform(req[1]), O = uniform(req[2]);
+            rw_stage_far<false>(mb + (int64_t)b * sstride, O, lane, swin[q & 1]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (the windows before the done word)
+            if (lane == 0) req[3] = q;
+            continue;
+        }
+        if (inflight)
+        {
+            spin = 0;
+            inflight = false;
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(pl), "+v"(tl)::"memory");  // the gathered letters
+            const int S = dg ? stab[pl * a.A + tl] : 0;
+            const int delta = lane <= ck ? a.gap * run + (dg ? -S : a.gap) : 0;
+            const int Pd = wave_prefix_sum(delta);
+            const int tot = __builtin_amdgcn_readlane(Pd, ck);
+            const int He = Hc + (tot - Pd);  // H at this lane's row entry
+            const int row = 64 * cb + lane + 1;
+            int rz = INT_MAX;  // the first cell r = 0 .. run of the row whose H = He + g r is 0
+            if (He == 0) rz = 0;
+            else if (a.gap < 0 && He % (-a.gap) == 0) rz = He / (-a.gap);
+            const bool e1 = rz <= run && rz < ce;                       // STOP before column 0
+            const bool e2 = !e1 && lv <= 0;                              // the LEFT run reaches column 0
+            const bool e3 = !e1 && !e2 && (row == 1 || (dg && lv == 1)); // TOP / DIAG onto row 0 / column 0
+            const uint64_t ev = ballot(lane <= ck && (e1 || e2 || e3));
+            if (ev == 0)
+            {
+                Hc += tot;
+                if (lane == 0) ctl[2] = cseen;
+                continue;
+            }
+            const int l = 63 - (int)__builtin_clzll(ev);  // the first in walk order (lane k down)
+            const int lrow = 64 * cb + l + 1;
+            const int lce = __builtin_amdgcn_readlane(ce, l), llv = __builtin_amdgcn_readlane(lv, l);
+            const int lrz = __builtin_amdgcn_readlane(rz, l), lrun = __builtin_amdgcn_readlane(run, l);
+            const bool l1 = (ballot(e1) >> l) & 1, l2 = (ballot(e2) >> l) & 1;
+            int nrec = cn0 + (ck - l), tail, st, sp0;
+            if (l1)
+            {
+                tail = lrz;  // the STOP cell (lrow, lce - lrz): every move into it updated the indices
+                st = lce - lrz - 1;
+                sp0 = lrow - 1;
+            }
+            else if (l2)
+            {
+                tail = lrun;  // LEFT moves to column 1, then onto column 0 without an index update
+                st = 0;
+                sp0 = lrow - 1;
+            }
+            else
+            {
+                nrec += 1;  // the row's record is whole; its move lands on the border (no index update)
+                tail = 0;
+                st = lrow == 1 ? llv - 1 : 0;
+                sp0 = lrow == 1 ? 0 : lrow - 1;
+            }
+            if (lane == 0)
+            {
+                ctl[4] = nrec;
+                ctl[5] = tail;
+                ctl[6] = st;
+                ctl[7] = sp0;
+                ctl[2] = cseen;
+                ctl[3] = 1;  // (after the fields: one wave's LDS writes execute in order)
+            }
+            ended = true;
+            continue;
+        }
+        if (!ended && uniform(ctl[0]) > cseen)
+        {
+            // take the next posted strip: its moves, entry columns, letters (gathers in flight)
+            spin = 0;
+            ++cseen;
+            const int *slot = chkBuf[cseen & 1];
+            const int pv = slot[lane];
+            cb = uniform(slot[64]);
+            ck = uniform(slot[65]);
+            const int jc = uniform(slot[66]);
+            cn0 = uniform(slot[67]);
+            if (cseen == 1) Hc = uniform(slot[68]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) ctl[1] = cseen;  // (the slot is free once read)
+            run = lane <= ck ? pv >> 1 : 0;
+            dg = lane <= ck ? pv & 1 : 0;
+            const int P = wave_prefix_sum(run + dg);
+            ce = jc - (__builtin_amdgcn_readlane(P, ck) - P);  // entry column of this lane's row
+            lv = ce - run;
+            pl = lane <= ck ? (int)a.pattern[poff + 64 * cb + lane] : 0;
+            tl = lane <= ck && dg && lv >= 1 ? (int)a.text[toff + lv - 1] : 0;
+            inflight = true;
+            continue;
+        }
+        if (spin > 64) __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 template <bool LOCAL>
 __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
 {
     __shared__ uint32_t pfbuf[2][kPfDw];
     __shared__ uint32_t swin[2][kStageWin * kWave];
     __shared__ int req[4];
+    __shared__ int stab[LOCAL ? 32 * 32 : 1];  // local: the substitution scores S (local_check)
+    // local: strips posted for local_check ([2][64 records + b, k, entry column, nrec before, H0]) and
+    // the check's control words ([0] posted, [1] taken, [2] done, [3] ended, [4..7] nrec, tail, starts)
+    __shared__ int chkBuf[LOCAL ? 2 : 1][72];
+    __shared__ int chkCtl[8];
     const int p = blockIdx.x;
     const int lane = threadIdx.x & (kWave - 1);
     if (threadIdx.x < 4) req[threadIdx.x] = 0;
+    if (threadIdx.x < 8) chkCtl[threadIdx.x] = 0;
+    if constexpr (LOCAL)
+        for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) stab[e] = a.score_tab[e] - a.gap;  // (the table holds S + g)
     __syncthreads();
     if (threadIdx.x >= kWave)
     {
@@ -516,7 +648,11 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
         if (uniform(sp.num_strips) > 0 && uniform((int)sp.text_len) > 0)
         {
             const StripDesc s0 = a.strips[uniform(sp.first_strip)];
-            rw_stager<LOCAL>(a, a.masks + uniform64(s0.mask_off) * 4, (int64_t)uniform(s0.nsteps) * 4, req, swin, lane);
+            if constexpr (LOCAL)
+                rw_stager_local(a, sp, a.masks + uniform64(s0.mask_off) * 4, (int64_t)uniform(s0.nsteps) * 4, req, swin,
+                                stab, chkBuf, chkCtl, lane);
+            else
+                rw_stager<false>(a, a.masks + uniform64(s0.mask_off) * 4, (int64_t)uniform(s0.nsteps) * 4, req, swin, lane);
         }
         return;
     }
@@ -539,6 +675,10 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
         int pfb = 0, pfclo = INT_MIN;
         int reqSeq = 0, reqO = 0;  // the last request to the stager
         Lines L;
+        // local: the walk runs on the global encoding (the R = 1 planes hold no STOP); after every
+        // strip it posts the strip's records to the stager wave, whose local_check finds where
+        // traceBackSW ends (rw_stager_local), and it stops once the stager reports the end
+        int chkSeq = 0;
         // expected column drift of the path per strip (prefetch placement)
         const int drift = (int)(((int64_t)n * 64 + m / 2) / m);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
@@ -600,9 +740,9 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             else
             {
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
-                rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W, sdbg);
+                rw_stage<false>(sb, pfbuf[pfb], pfclo, jo, lane, W, sdbg);
 #else
-                rw_stage<LOCAL>(sb, pfbuf[pfb], pfclo, jo, lane, W);
+                rw_stage<false>(sb, pfbuf[pfb], pfclo, jo, lane, W);
 #endif
             }
             // the next strip's windows: the stager builds them while this strip is walked
@@ -648,13 +788,13 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
                 ++nRestage;
 #endif
-                rw_stage<LOCAL>(sb, pfbuf[pfb], INT_MIN, jo, lane, W);
+                rw_stage<false>(sb, pfbuf[pfb], INT_MIN, jo, lane, W);
             };
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             asm volatile("" : "+v"(W[0]));
             const uint64_t c1 = __builtin_amdgcn_s_memtime();
 #endif
-            walk_batch<LOCAL>(L, a.fast != 0, 0, W, restage);
+            walk_batch<false>(L, a.fast != 0, 0, W, restage);
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
             const uint64_t c2 = __builtin_amdgcn_s_memtime();
             tStage += c1 - c0;
@@ -663,6 +803,42 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             // records of rows k .. kend (record index: rows walked before + k - lane)
             const int kend = L.stopped ? L.stopLane + 1 : 0;
             if (lane >= kend && lane <= k) rec[nrec + k - lane] = (int32_t)L.vrec;
+            if constexpr (LOCAL)
+            {
+                // post this strip to the stager's check (slot chkSeq & 1, free once the stager has
+                // taken the check two before); one wave's LDS writes execute in order, so the records
+                // and the header are there when the sequence word is
+                ++chkSeq;
+                // (the stager takes no checks once the walk has ended: stop waiting for the slot then)
+                bool over = false;
+                for (uint32_t spin = 1; uniform(((volatile int *)chkCtl)[1]) < chkSeq - 2; ++spin)
+                {
+                    if ((over = uniform(((volatile int *)chkCtl)[3]) != 0)) break;
+                    if (spin > 16) __builtin_amdgcn_s_sleep(1);
+                    if (spin > (1u << 26)) break;  // (never: the stager always takes or ends; a bound, not a wait)
+                }
+                if (over)
+                {
+                    nrec += k - kend + 1;
+                    break;
+                }
+                int *slot = chkBuf[chkSeq & 1];
+                slot[lane] = (int)L.vrec;
+                if (lane == 0)
+                {
+                    slot[64] = b;
+                    slot[65] = k;
+                    slot[66] = jc;
+                    slot[67] = nrec;
+                    slot[68] = h.score;  // (the first check's H at the start cell)
+                    ((volatile int *)chkCtl)[0] = chkSeq;
+                }
+                if (uniform(((volatile int *)chkCtl)[3]) != 0)
+                {
+                    nrec += k - kend + 1;
+                    break;  // the path ended in a strip already checked
+                }
+            }
             nrec += k - kend + 1;
             if (L.stopped)
             {
@@ -689,7 +865,6 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             pfb ^= 1;
             pfclo = pfnext;
         }
-        h.nrec = nrec;
 #if defined(SA_EXPERIMENT) && defined(SA_EXP_WALK_TIMING)
         if (a.timing && lane == 0)
         {
@@ -703,20 +878,29 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
             a.timing[8 * (size_t)gridDim.x + (size_t)p] = nStagerHit;
         }
 #endif
-        if (!L.stopped)
+        if constexpr (!LOCAL)
         {
-            if constexpr (!LOCAL)
+            h.nrec = nrec;
+            if (!L.stopped)
             {
                 h.tail = jc;  // row 0: LEFT to column 0 (traceBackNW :80-81)
                 h.start_text = 0;
                 h.start_pattern = 0;
             }
-            else
+        }
+        else
+        {
+            // the stager's verdict (the last strip posted is strip 0 at the latest, whose row 1 always
+            // ends the walk)
+            for (uint32_t spin = 1; uniform(((volatile int *)chkCtl)[3]) == 0; ++spin)
             {
-                // row 0 reached from row 1, whose leaving cell is column jc + DIAG
-                h.start_text = jc + (L.lastp & 1) - 1;
-                h.start_pattern = 0;
+                if (spin > 16) __builtin_amdgcn_s_sleep(1);
+                if (spin > (1u << 26)) break;  // (a bound, never reached: strip 0's check always ends the walk)
             }
+            h.nrec = ((volatile int *)chkCtl)[4];
+            h.tail = ((volatile int *)chkCtl)[5];
+            h.start_text = ((volatile int *)chkCtl)[6];
+            h.start_pattern = ((volatile int *)chkCtl)[7];
         }
     }
     if (lane == 0)

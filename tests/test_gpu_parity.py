@@ -200,7 +200,10 @@ def test_batch_plan_config5(eng, golden):
 @pytest.mark.parametrize("mode", [0, 1])
 def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane, gap):
     """The fill alone, cell by cell: the engine's DIRECTION matrix (decoded from its bit-planes) equals
-    the reference's (m+1)x(n+1) byte matrix M (alignSequenceCPU.cpp:116-284) on every cell."""
+    the reference's (m+1)x(n+1) byte matrix M (alignSequenceCPU.cpp:116-284) on every cell. Local
+    plans with one row per lane store no STOP bit: every interior cell is compared with the
+    reference's decision before its STOP override (:181-189; oracle mode 2), and the STOP cells -- the
+    cells whose score is 0 -- are the traceback's (the alignment tests)."""
     from sa_amd.batch import DeviceBatch
     S = synthetic.blast_matrix()
     for k, (n, m) in enumerate([(1500, 1400), (700, 700), (130, 66)]):
@@ -210,7 +213,7 @@ def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane, gap):
         b.fill()
         got = b.directions(0)
         exp = np.empty((m + 1) * (n + 1), np.uint8)
-        oracle.fill_only(mode, t, p, S, gap, exp)
+        oracle.fill_only(2 if mode == 1 and rows_per_lane == 1 else mode, t, p, S, gap, exp)
         bad = int((got != exp).sum())
         b.close()
         assert bad == 0, (n, m, bad)
@@ -281,7 +284,7 @@ def test_chain_ring_laps_across_groups(eng, mode):
     for k in (1, 4):
         n, m = shapes[k]
         exp = np.empty((m + 1) * (n + 1), np.uint8)
-        oracle.fill_only(mode, texts[k], pats[k], S, 5, exp)
+        oracle.fill_only(2 if mode == 1 else 0, texts[k], pats[k], S, 5, exp)  # (local: raw decisions)
         assert int((b.directions(k) != exp).sum()) == 0, shapes[k]
     b.close()
 

@@ -79,3 +79,24 @@ def test_oracle_matches_reference_binary_on_fresh_inputs():
         jobs.append((k % 2, t, p, S, int(rng.integers(-6, 12))))
     for job, r in zip(jobs, oracle.ref_align_batch(jobs)):
         assert oracle.align(*job) == r
+
+
+def test_oracle_local_raw_decisions():
+    """(CPU) oracle mode 2 (the engine's rows_per_lane 1 local planes): every interior cell holds the
+    reference's decision before its STOP override (alignSequenceCPU.cpp:181-189), so it equals mode 1
+    wherever mode 1 is not STOP, and the border rows stay STOP."""
+    import numpy as np
+    from sa_amd import synthetic
+    S = synthetic.blast_matrix()
+    t = synthetic.random_sequence(11, 300, 4)
+    p = synthetic.mutate(t, 12, 4, 280)
+    n, m = len(t), len(p)
+    loc = np.empty((m + 1) * (n + 1), np.uint8)
+    raw = np.empty_like(loc)
+    oracle.fill_only(1, t, p, S, 5, loc)
+    oracle.fill_only(2, t, p, S, 5, raw)
+    loc, raw = loc.reshape(m + 1, n + 1), raw.reshape(m + 1, n + 1)
+    keep = loc != 3
+    assert (raw[keep] == loc[keep]).all()
+    assert (raw[1:, 1:] != 3).all() and (raw[0] == 3).all() and (raw[:, 0] == 3).all()
+    assert (loc[1:, 1:] == 3).any()  # the case has STOP cells

@@ -7,7 +7,7 @@ import re
 import sys
 
 S = open(sys.argv[1]).read().split("\n")
-for name in ("_ZN2sa11fill_kernelILi1ELb0ELi3ELb1EEEvNS_8FillArgsE", "_ZN2sa11fill_kernelILi1ELb1ELi3ELb1EEEvNS_8FillArgsE"):
+for name in ("_ZN2sa11fill_kernelILi1ELb0ELi3ELb1ELb0EEEvNS_8FillArgsE", "_ZN2sa11fill_kernelILi1ELb1ELi3ELb1ELb0EEEvNS_8FillArgsE"):
     st = [i for i, l in enumerate(S) if l.startswith(name + ":")][0]
     en = [i for i in range(st, len(S)) if S[i].startswith(".Lfunc_end")][0]
     L = S[st:en]

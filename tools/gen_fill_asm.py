@@ -20,17 +20,16 @@ One step (four registers rotate through the roles Qn -> Q/up -> diag/F' -> left,
         (F' goes to the diag register, dead after d)
     g   X[4h + (k & 3)] byte 3 - (k >> 2) = M - D     (SDWA, other bytes kept: sign = DIAG)
     h   Y[4h + (k & 3)] byte 3 - (k >> 2) = left - up  (sign = raw "up > left" / raw TOP)
-    i   local: Z[4h + (k & 3)] byte 3 - (k >> 2) = ffbh(F')  (0xff = STOP: ffbh(0) = -1, else <= 31)
 with k the step in the body and h = HALF the body's word of the 32-slot chunk. A difference's low
 byte has the sign of the difference when the difference lies in [-128, 127]: the plan uses these
 bodies only when every difference is bounded so (sa_engine.hip, byte_diffs). The R = 1 plane word
 is INTERLEAVED (sa_layout.h): slot k of a word has DIAG at bit 31 - 2k and the second plane at bit
 30 - 2k, so register r = 4h + t0 (steps t0, t0 + 4, t0 + 8, t0 + 12 in bytes 3..0) lands with one
 shift: (X[r] & 0x80808080) >> 2 t0, (Y[r] & 0x80808080) >> (2 t0 + 1). The merge costs 15 VALU per
-word (global) and the sign bits 1 VALU per bit: about 2.94 VALU per step for two bits instead of 4
-(one subtraction and one v_alignbit per bit). Local: STOP bytes are 0xff, so (Z & 0xc0c0c0c0) >> 2 t0
-sets both bits of a STOP cell, and word = A | (B & ~(A >> 1)) with A = DIAG|STOP (odd bits) + STOP
-(even bits) and B = raw TOP (even bits) is plane 1 = (TOP & ~DIAG) | STOP: 24 VALU per word.
+word and the sign bits 1 VALU per bit: about 2.94 VALU per step for two bits instead of 4 (one
+subtraction and one v_alignbit per bit). Local stores the same two bits (DIAG, raw TOP): a STOP cell
+is one whose H is 0, and the row walk recomputes H along the path (sa_walk.hip), so the planes need
+no third bit (round 4 spent an ffbh per step and 9 more merge VALU per word on it).
 A global step is 7 VALU ops (plus the merge) with or without a strip below: the queue's
 bottom-row values run one step later than the C++ bodies' (whose Qn takes F of the previous step
 through a register copy), and the publish at the body's end shifts the queue once more with F of
@@ -103,8 +102,8 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
             out.append(f"v_subrev_u32_e32 {dg}, {G}, {XR}")
             kreg = KEY if k % 2 == 0 else KEY2
             out.append(f"v_lshl_add_u32 {kreg}, {dg}, {KB}, {-q}")
-            # STOP: ffbh(H) is 0xffffffff for H == 0 and at most 31 otherwise: bit 7 of its low byte
-            out.append(f"v_ffbh_u32_sdwa {Z[g]}, {dg} dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD")
+            # (no STOP bits: a cell is STOP exactly when its H is 0, and the traceback follows H along
+            # the path from the best cell's score, sa_walk.hip local_check)
             if k % 2 == 1:
                 out.append(f"v_max3_i32 {BM}, {BM}, {KEY}, {KEY2}")
     if hp:
@@ -193,7 +192,10 @@ def band_operands(local: bool, hn: bool, hp: bool):
 
 
 def merge(local: bool) -> str:
-    """The chunk's sign bits into its two interleaved words a0 (slots 0..15), a1 (slots 16..31)."""
+    """The chunk's sign bits into its two interleaved words a0 (slots 0..15), a1 (slots 16..31). Both
+    modes store DIAG and the raw "up > left" (local: raw TOP) bits; local STOP is H == 0, which the
+    traceback recomputes, so the local merge is the global one."""
+    local = False
     out = []
     for h, acc in ((0, "%[a0]"), (1, "%[a1]")):
         # (register, shift, mask operand) terms of the word's DIAG|STOP accumulator and of its TOP one
@@ -232,7 +234,6 @@ def operands(local: bool, hn: bool, hp: bool):
     outs += [f'[x{g}] "+v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "+v"(r.Y[{g}])' for g in range(8)]
     ins = [f'[tw{i}] "v"(r.T[{i}])' for i in range(4)]
     if local:
-        outs += [f'[z{g}] "+v"(r.Z[{g}])' for g in range(8)]
         outs += ['[bm] "+v"(r.bm)', '[xr] "=&v"(Xr)', '[key] "=&v"(key)', '[key2] "=&v"(key2)']
         ins += ['[g] "s"(r.g)', '[kb] "s"(r.kb)']
     if hp:
@@ -294,9 +295,6 @@ def main():
         outs = ['[a0] "=&v"(r.acc0)', '[a1] "=&v"(r.acc1)', '[tx] "=&v"(tx)']
         ins = [f'[x{g}] "v"(r.X[{g}])' for g in range(8)] + [f'[y{g}] "v"(r.Y[{g}])' for g in range(8)]
         ins += [f'[mk{g}] "v"(r.mk[{g}])' for g in range(8)]
-        if local:
-            outs += ['[tb] "=&v"(tb)']
-            ins += [f'[z{g}] "v"(r.Z[{g}])' for g in range(8)] + [f'[mz{t}] "v"(r.mz[{t}])' for t in range(4)]
         lines.append(f"template <> __device__ __forceinline__ void merge_asm<{str(local).lower()}>(StepRegs &r)")
         lines.append("{")
         lines.append("    int tx, tb;")
