@@ -193,7 +193,7 @@ struct Knobs {
     bool no_pair16 = false;         // SA_NO_PAIR16: disable the pair-packed batch fill
     int band = -1;                  // SA_BAND: 1 / 0 force the band fill (128-row score strips
                                     // feeding the 64-row strips, sa_fill.hip process_band) on / off
-                                    // (1 also past kBandPersistRows); default: on wherever it applies
+                                    // (1 also past kBandPersistRows*); default: on wherever it applies
                                     // (plan_create)
     double handoff_timeout_s = 20;  // SA_HANDOFF_TIMEOUT_S: in-kernel hand-off give-up time
     int io_sleep = 4;               // SA_IO_SLEEP: I/O wave idle poll period (s_sleep units)
@@ -203,6 +203,9 @@ struct Knobs {
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
     bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
     int max_cus = 0;                // SA_MAX_CUS: plan as if the device had at most this many CUs (tests)
+    int chain_per_cu = 0;           // SA_CHAIN_PER_CU: 1 / 2 chain workgroups per CU (default: plan_create)
+    int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
+                                    // capacity (default kBandPersistRows*)
 };
 
 const Knobs &knobs()
@@ -223,6 +226,8 @@ const Knobs &knobs()
         v.tb_generic = get("SA_TB_GENERIC") != nullptr;
         if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
         if (const char *e = get("SA_MAX_CUS")) v.max_cus = std::max(0, std::atoi(e));
+        if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
+        if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         return v;
     }();
     return k;
@@ -284,6 +289,7 @@ struct sa_plan {
     int mode = 0, A = 0, gap = 0, R = 0, U = 0, W = 1, key_bits = 12, key_rowbits = 21;
     int sk = 0;          // ScoreKind of the fill
     bool chain = false;  // some pair has more than one strip
+    bool chain_solo = false;  // one chain workgroup per CU (one compute wave per SIMD), see plan_create
     // band fill (R = 1 int8-profile chains): 128-row score strips ahead of the 64-row strips
     bool band = false;
     std::vector<StripDesc> bands;
@@ -346,7 +352,9 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
 
 // Waves per workgroup (strips per group). Chains of strips (pairs taller than one strip) hand
 // their rows off through LDS inside a group; single-strip pairs gain nothing from grouping.
-constexpr int64_t kBandPersistRows = 320000;  // band fill with persistent workers up to this many rows (measured: +12 % at 250000^2, -16 % at 500000^2)
+// band fill with persistent workers up to this many rows (DNA-sized alphabets / larger ones); past
+// them the one-wave fill with one workgroup per CU is ahead (profiles/r05/ab_chain_per_cu_v0.log, ab_chain_solo_v1.log)
+constexpr int64_t kBandPersistRows = 90112, kBandPersistRowsWide = 65536;
 
 int choose_W(const std::vector<PairDesc> &pairs)
 {
@@ -763,8 +771,9 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         // on top of the strips' costs more than their shorter ramp saves
         int64_t mmax = 0;
         for (const PairDesc &d : pl->pairs) mmax = std::max<int64_t>(mmax, (int64_t)d.pattern_len);
+        const int64_t persistRows = knobs().band_rows > 0 ? knobs().band_rows : (A <= 4 ? kBandPersistRows : kBandPersistRowsWide);
         band = band && nb > 0 &&
-               (stripGroups + bandGroups <= pl->num_cu || ((mmax <= kBandPersistRows || knobs().band == 1) && pl->num_cu >= 4));
+               (stripGroups + bandGroups <= pl->num_cu || ((mmax <= persistRows || knobs().band == 1) && pl->num_cu >= 4));
         if (band)
         {
             // bands b = 0 .. B-2 of each pair (B = ceil(strips / 2); the last band's bottom row feeds
@@ -799,6 +808,16 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             }
             pl->band = true;
         }
+    }
+    {
+        // one-wave chain fill: a second workgroup on a CU puts two compute waves on a SIMD, which
+        // raises the step time 25 -> 41 ns and the hand-off lag 2.5 -> 4.6 us (tools/timeline.py,
+        // 120000^2); the strip chains of a few long pairs are latency-bound (a strip starts one lag
+        // after the one above), so they get one workgroup per CU; many chained pairs keep two
+        int64_t chained = 0;
+        for (const PairDesc &d : pl->pairs) chained += d.num_strips > 1;
+        pl->chain_solo = pl->chain && !pl->band && chained < pl->num_cu;
+        if (knobs().chain_per_cu) pl->chain_solo = pl->chain && !pl->band && knobs().chain_per_cu == 1;
     }
 
     // ---- tables ----
@@ -1009,6 +1028,12 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const int units = ns / 2;
             a.num_groups = (units + W - 1) / W;
             grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
+        }
+        if (pl->chain_solo)
+        {
+            // (plan_create) an LDS request above half a CU's keeps a second workgroup off the CU
+            a.chain_lds = std::max(a.chain_lds, 96 * 1024);
+            grid = std::min(a.num_groups, std::max(1, pl->num_cu));
         }
         if (pl->band)
         {

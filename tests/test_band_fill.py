@@ -130,6 +130,14 @@ def test_band_fill_persistent_workers_vs_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("per_cu", ["1", "2"])
+def test_one_wave_chain_fill_per_cu_vs_oracle(per_cu):
+    """The same plans without bands (SA_BAND=0): 32 strip groups on 16 CUs with one chain workgroup
+    per CU (the default for a few long pairs, a 96 KB LDS request) or two; cell by cell as above."""
+    _run(PERSIST, SA_MAX_CUS="16", SA_BAND="0", SA_CHAIN_PER_CU=per_cu)
+
+
+@pytest.mark.gpu
 def test_local_then_global_32k_fresh_process():
     _run(LARGE)
 

@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pairs", type=int, default=1, help="independent copies of the pair (contention test)")
     ap.add_argument("--score", default="blast", help="blast (+5/-4) or MATCH,MISMATCH (e.g. 1,-3)")
+    ap.add_argument("--protein", action="store_true", help="BLOSUM50, letters 0..21 (the harness's dummy requests)")
     args = ap.parse_args()
     if args.waves:
         os.environ["SA_WAVES_PER_GROUP"] = str(args.waves)
@@ -97,8 +98,13 @@ def main():
         mt, mm = (int(x) for x in args.score.split(","))
         S = np.full((4, 4), mm, dtype=np.int32)
         np.fill_diagonal(S, mt)
-    t = synthetic.random_sequence(6, args.n, 4)
-    p = synthetic.random_sequence(7, args.m, 4)
+    A = 4
+    if args.protein:
+        S = np.array(json.load(open(os.path.join(ROOT, "tests", "golden", "matrices.json")))["blosum50"],
+                     np.int32).reshape(23, 23)
+        A = 22
+    t = synthetic.random_sequence(6, args.n, A)
+    p = synthetic.random_sequence(7, args.m, A)
     b = DeviceBatch(args.mode, S, 5, [t] * args.pairs, [p] * args.pairs, rows_per_lane=args.R)
     b.fill()
     b.fill()
