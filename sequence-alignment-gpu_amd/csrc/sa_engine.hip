@@ -202,6 +202,9 @@ struct Knobs {
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
     bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
+    bool tb_tables = true;          // SA_TB_TABLES=0: no table traceback (every pair walks sequentially)
+    bool tb_strict = false;         // SA_TB_STRICT: no sequential walk after the table traceback
+                                    // (tests: a pair it left keeps a stale head and fails its check)
     int max_cus = 0;                // SA_MAX_CUS: plan as if the device had at most this many CUs (tests)
     int chain_per_cu = 0;           // SA_CHAIN_PER_CU: 1 / 2 chain workgroups per CU (default: plan_create)
     int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
@@ -225,6 +228,8 @@ const Knobs &knobs()
         v.tb_timing = get("SA_TB_TIMING");
         v.tb_generic = get("SA_TB_GENERIC") != nullptr;
         if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
+        if (const char *e = get("SA_TB_TABLES")) v.tb_tables = std::atoi(e) != 0;
+        v.tb_strict = get("SA_TB_STRICT") != nullptr;
         if (const char *e = get("SA_MAX_CUS")) v.max_cus = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
@@ -312,6 +317,11 @@ struct sa_plan {
     Control *d_ctrl = nullptr;
     int32_t *d_rec = nullptr;  // traceback records (sa_walk.h)
     TbHead *d_heads = nullptr;
+    // table traceback (sa_walk.h TbArgs; R = 1 global plans with a pair of kTbMinStrips strips or more)
+    std::vector<TbGroup> tb_groups;
+    std::vector<int32_t> tb_pg;  // [np + 1] first group of each pair
+    TbGroup *d_tbgroups = nullptr;
+    int32_t *d_tbpg = nullptr, *d_tbl = nullptr, *d_gtbl = nullptr, *d_gent = nullptr, *d_tbflag = nullptr;
     char *d_out_text = nullptr, *d_out_pattern = nullptr;
     sa_result *d_results = nullptr;
     const int8_t *d_text_in = nullptr, *d_pattern_in = nullptr;
@@ -386,7 +396,8 @@ void free_plan(sa_plan *p)
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
-                    p->d_out_pattern, p->d_results, p->d_bands};
+                    p->d_out_pattern, p->d_results, p->d_bands, p->d_tbgroups, p->d_tbpg, p->d_tbl,
+                    p->d_gtbl, p->d_gent, p->d_tbflag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -833,6 +844,23 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             prof[cp] = (int32_t)w;
         }
 
+    // ---- table traceback groups (sa_walk.h) ----
+    if (pl->R == 1 && P->mode == SA_GLOBAL && knobs().tb_tables)
+    {
+        pl->tb_pg.assign(np + 1, 0);
+        for (int64_t p = 0; p < np; ++p)
+        {
+            const PairDesc &d = pl->pairs[p];
+            pl->tb_pg[p] = (int32_t)pl->tb_groups.size();
+            if (d.num_strips < kTbMinStrips || d.text_len == 0) continue;
+            for (int s = 0; s < d.num_strips; s += kTbG)
+                pl->tb_groups.push_back({(int32_t)p, d.first_strip + s, d.first_strip + std::min(d.num_strips, s + kTbG) - 1, 0});
+        }
+        pl->tb_pg[np] = (int32_t)pl->tb_groups.size();
+        if (pl->tb_groups.empty()) pl->tb_pg.clear();
+    }
+    const size_t ntg = pl->tb_groups.size();
+
     // ---- device buffers ----
     const size_t nstr = std::max<size_t>(1, pl->strips.size()), npp = std::max<size_t>(1, np);
     const size_t codeB = 4 * code_bytes + 16, bndB = granules * 8 + 16, bestB = sizeof(uint64_t) * nstr;
@@ -846,6 +874,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_prof, sizeof(int32_t) * 4},
         {(void **)&pl->d_table, sizeof(int32_t) * A * A},
         {(void **)&pl->d_bands, sizeof(StripDesc) * pl->bands.size()},
+        {(void **)&pl->d_tbgroups, sizeof(TbGroup) * ntg},
+        {(void **)&pl->d_tbpg, ntg ? sizeof(int32_t) * (np + 1) : 0},
         {(void **)&pl->d_ws_text, in ? inN + 16 : 0},
         {(void **)&pl->d_ws_pattern, in ? inM + 16 : 0},
         {(void **)&pl->d_ctrl, sizeof(Control)},
@@ -860,6 +890,10 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_score, sizeof(int32_t) * npp},
         {(void **)&pl->d_rec, 4 * recw + 16},
         {(void **)&pl->d_heads, sizeof(TbHead) * npp},
+        {(void **)&pl->d_tbl, ntg ? sizeof(int32_t) * kTbK * nstr : 0},
+        {(void **)&pl->d_gtbl, sizeof(int32_t) * kTbK * ntg},
+        {(void **)&pl->d_gent, sizeof(int32_t) * ntg},
+        {(void **)&pl->d_tbflag, ntg ? sizeof(int32_t) * npp : 0},
     };
     int rc = SA_OK;
     if (ws)
@@ -898,6 +932,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         put(pl->d_prof, prof.data(), sizeof(int32_t) * 4);
         put(pl->d_table, table.data(), sizeof(int32_t) * A * A);
         put(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size());
+        put(pl->d_tbgroups, pl->tb_groups.data(), sizeof(TbGroup) * ntg);
+        if (ntg) put(pl->d_tbpg, pl->tb_pg.data(), sizeof(int32_t) * (np + 1));
         put(pl->d_ws_text, in->text, inN);
         put(pl->d_ws_pattern, in->pattern, inM);
         std::memset(h + ((char *)pl->d_ctrl - pl->d_up), 0, sizeof(Control));
@@ -926,6 +962,9 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
     if (okc && pl->band)
         okc = hipMemcpyAsync(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size(), hipMemcpyHostToDevice, st) == hipSuccess;
+    if (okc && ntg)
+        okc = hipMemcpyAsync(pl->d_tbgroups, pl->tb_groups.data(), sizeof(TbGroup) * ntg, hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemcpyAsync(pl->d_tbpg, pl->tb_pg.data(), sizeof(int32_t) * (np + 1), hipMemcpyHostToDevice, st) == hipSuccess;
     // a plan of its own is complete when sa_plan_create returns (callers fill on other streams)
     if (okc) okc = hipStreamSynchronize(st) == hipSuccess;
     if (!okc) { free_plan(pl); restore(); return fail(SA_ERR_HIP, "plan upload failed"); }
@@ -1110,7 +1149,30 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     w.pattern = pl->d_pattern_in;
     w.score_tab = pl->d_table;
     w.A = pl->A;
-    launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
+    w.tb_flag = nullptr;
+    if (!pl->tb_groups.empty())
+    {
+        // table traceback first; the sequential walk then takes only the pairs it left (tb_flag)
+        TbArgs t;
+        t.strips = pl->d_strips;
+        t.pairs = pl->d_pairs;
+        t.masks = pl->d_masks;
+        t.groups = pl->d_tbgroups;
+        t.pair_g0 = pl->d_tbpg;
+        t.pair_score = pl->d_score;
+        t.tbl = pl->d_tbl;
+        t.gtbl = pl->d_gtbl;
+        t.gent = pl->d_gent;
+        t.tb_flag = pl->d_tbflag;
+        t.rec = pl->d_rec;
+        t.heads = pl->d_heads;
+        t.fast = w.fast;
+        launch_tb(t, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, st);
+        HIP_TRY(hipGetLastError());
+        if (int rc = debug_sync(st, "table traceback")) return rc;
+        w.tb_flag = pl->d_tbflag;
+    }
+    if (!w.tb_flag || !kn.tb_strict) launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "walk kernel")) return rc;
     ExpandArgs x;

@@ -47,7 +47,50 @@ struct WalkArgs {
     const int8_t *text, *pattern;  // the fill's inputs (alphabet indices)
     const int32_t *score_tab;      // A x A, S + g (the plan's local table)
     int32_t A;
+    // table traceback (R = 1, see TbGroup): walk_rw_kernel walks only the pairs whose tb_flag is set
+    const int32_t *tb_flag;        // null: every pair
 };
+
+// TABLE TRACEBACK (R = 1 global plans; sa_walk.hip tb_*_kernel). The sequential walk of a long pair
+// costs ~60 clk per row on one wave. Instead every strip b gets a TABLE: for each start column c of
+// a window of kTbK columns (tb_window_lo) the column at which the walk entering the strip's last row
+// at c enters the row above the strip (one lane per start column, all strips at once). Groups of kTbG
+// strips compose their tables; one wave per pair chains the group tables from (m, n) upward, which
+// gives every group's entry column, and each group then chains its strips' tables and walks its
+// strips in parallel (one wave each, the row walk's code), writing the records by row. A start
+// column outside a window ends the chain: the pair falls back to walk_rw_kernel (tb_flag).
+constexpr int kTbK = 2048;       // start columns per strip window
+constexpr int kTbG = 16;         // strips per group
+constexpr int kTbMinStrips = 8;  // pairs with fewer strips take the sequential walk
+struct TbGroup {
+    int32_t pair, s_lo, s_hi, pad;  // the plan's strip indices, s_lo <= s_hi (one pair's)
+};
+struct TbArgs {
+    const StripDesc *strips;
+    const PairDesc *pairs;
+    const uint32_t *masks;
+    const TbGroup *groups;
+    const int32_t *pair_g0;  // [np + 1]: pair p's groups are pair_g0[p] .. pair_g0[p + 1] - 1
+    const int32_t *pair_score;
+    int32_t *tbl;            // [strip][kTbK] exit column (-1: start column past n)
+    int32_t *gtbl;           // [group][kTbK] exit column of the group (-1: left a window)
+    int32_t *gent;           // [group] entry column (tb_resolve_kernel)
+    int32_t *tb_flag;        // [pair] 1: walk_rw_kernel walks the pair
+    int32_t *rec;
+    TbHead *heads;
+    int32_t fast;
+};
+
+// First column of strip b's window (pair of n columns, m rows): kTbK columns centred on the diagonal
+// through (m, n) at the strip's last row (host and device)
+__host__ __device__ inline int tb_window_lo(int b, int n, int m)
+{
+    const int64_t r = b * 64 + 64 < m ? b * 64 + 64 : m;
+    const int64_t c = (r * n + m / 2) / m - kTbK / 2;
+    const int64_t hi = n + 1 - kTbK > 0 ? n + 1 - kTbK : 0;
+    return (int)(c < 0 ? 0 : (c > hi ? hi : c));
+}
+void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st);
 
 struct ExpandArgs {
     const int8_t *text, *pattern;

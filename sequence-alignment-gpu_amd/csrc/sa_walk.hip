@@ -635,6 +635,7 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
     __shared__ int chkBuf[LOCAL ? 2 : 1][72];
     __shared__ int chkCtl[8];
     const int p = blockIdx.x;
+    if (a.tb_flag && uniform(a.tb_flag[p]) == 0) return;  // (the table traceback walked the pair)
     const int lane = threadIdx.x & (kWave - 1);
     if (threadIdx.x < 4) req[threadIdx.x] = 0;
     if (threadIdx.x < 8) chkCtl[threadIdx.x] = 0;
@@ -1060,6 +1061,191 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 }
 
 // ------------------------------------------------------------------------------------------------
+// table traceback (R = 1 global; sa_walk.h TbArgs)
+// ------------------------------------------------------------------------------------------------
+constexpr int kTbMargin = 320;                            // columns staged left of a window
+constexpr int kTbChunks = (kTbK + 63 + kTbMargin) / 32 + 2;  // R = 1 chunks staged per strip
+constexpr int kTbStride = kChunkDw + 4;                   // LDS dwords per chunk (padded: chunks on other banks)
+
+// Word of strip lane k holding slot e (R = 1 interleaved planes, sa_layout.h): the staged copy when it
+// holds the chunk, else global memory
+__device__ __forceinline__ uint32_t tb_word(const uint32_t *buf, int clo, int nch, const uint32_t *sb, int k, int e)
+{
+    const int c = e >> 5, off = k * 2 + ((e >> 4) & 1);
+    return (unsigned)(c - clo) < (unsigned)nch ? buf[(c - clo) * kTbStride + off] : sb[(int64_t)c * kChunkDw + off];
+}
+
+// One row of traceBackNW (alignSequenceCPU.cpp:64-114) from entry column j of strip lane k: LEFT while
+// the cell is LEFT, then TOP or DIAG out of the row; column 0 is TOP (:78-79). Slot s of a word sits
+// at bits 31 - 2s (plane 0, DIAG) and 30 - 2s (plane 1, up > left): the cell is not LEFT where either
+// is set, and the nearest such cell at or left of column j is the lowest set bit at or above 30 - 2s.
+// Returns the entry column of the row above.
+__device__ __forceinline__ int tb_row(int j, int k, const uint32_t *buf, int clo, int nch, const uint32_t *sb)
+{
+    while (j > 0)
+    {
+        const int e = j - 1 + k;
+        const uint32_t x = tb_word(buf, clo, nch, sb, k, e);
+        const int s = e & 15;
+        const uint32_t y = (x | (x >> 1)) & 0x55555555u & (0xffffffffu << (30 - 2 * s));
+        if (y)
+        {
+            const int q = __builtin_ctz(y);
+            return j - (s - ((30 - q) >> 1)) - (int)((x >> (q + 1)) & 1u);
+        }
+        j -= s + 1;  // a LEFT run past this word
+    }
+    return 0;
+}
+
+// Strip tables: block = one strip, 1024 threads x 2 start columns (the window), the strip's planes
+// around the window staged in LDS; rows from the strip's last down to its first
+__global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
+{
+    __shared__ uint32_t buf[kTbChunks * kTbStride];
+    const int s = blockIdx.x;
+    const StripDesc sd = a.strips[s];
+    const int p = uniform(sd.pair);
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p])) return;  // (a pair of the sequential walk)
+    const PairDesc pd = a.pairs[p];
+    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
+    const int b = s - uniform(pd.first_strip);
+    const int kTop = min(63, m - 1 - 64 * b);
+    const int lo = tb_window_lo(b, n, m);
+    const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
+    const int clo = max(0, (lo - 1 - kTbMargin) >> 5);
+    const int nch = max(0, min(kTbChunks, (uniform(sd.nsteps) >> 5) - clo));
+    for (int e = threadIdx.x; e < nch * (kChunkDw / 4); e += blockDim.x)
+    {
+        const int q = e / (kChunkDw / 4), r = e % (kChunkDw / 4);
+        *reinterpret_cast<uint4 *>(&buf[q * kTbStride + 4 * r]) =
+            *reinterpret_cast<const uint4 *>(sb + ((int64_t)clo + q) * kChunkDw + 4 * r);
+    }
+    __syncthreads();
+    const int c0 = lo + (int)threadIdx.x, c1 = c0 + 1024;
+    int x0 = c0 <= n ? c0 : 0, x1 = c1 <= n ? c1 : 0;
+    for (int k = kTop; k >= 0; --k)
+    {
+        x0 = tb_row(x0, k, buf, clo, nch, sb);
+        x1 = tb_row(x1, k, buf, clo, nch, sb);
+    }
+    int32_t *out = a.tbl + (int64_t)s * kTbK;
+    out[threadIdx.x] = c0 <= n ? x0 : -1;
+    out[threadIdx.x + 1024] = c1 <= n ? x1 : -1;
+}
+
+// Group tables: the strip tables of the group chained from its last strip to its first, per start
+// column of the last strip's window (-1 once a column leaves a window)
+__global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
+{
+    const TbGroup g = a.groups[blockIdx.x];
+    const PairDesc pd = a.pairs[uniform(g.pair)];
+    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len), first = uniform(pd.first_strip);
+    const int sLo = uniform(g.s_lo), sHi = uniform(g.s_hi);
+    const int loHi = tb_window_lo(sHi - first, n, m);
+    for (int t = threadIdx.x; t < kTbK; t += blockDim.x)
+    {
+        int x = loHi + t <= n ? loHi + t : -1;
+        for (int s = sHi; s >= sLo && x >= 0; --s)
+        {
+            const int lo = tb_window_lo(s - first, n, m);
+            x = (x >= lo && x < lo + kTbK) ? a.tbl[(int64_t)s * kTbK + x - lo] : -1;
+        }
+        a.gtbl[(int64_t)blockIdx.x * kTbK + t] = x;
+    }
+}
+
+// One wave per pair: the group tables chained from (m, n) upward give every group's entry column and
+// the row-0 column (the trailing LEFT run); the pair's head. A column outside a window: tb_flag = 1
+// and walk_rw_kernel walks the pair instead.
+__global__ __launch_bounds__(64) void tb_resolve_kernel(TbArgs a)
+{
+    const int p = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    const int g0 = a.pair_g0[p], g1 = a.pair_g0[p + 1];
+    if (g1 == g0)
+    {
+        a.tb_flag[p] = 1;
+        return;
+    }
+    const PairDesc pd = a.pairs[p];
+    const int n = (int)pd.text_len, m = (int)pd.pattern_len, first = pd.first_strip;
+    int x = n;
+    for (int g = g1 - 1; g >= g0; --g)
+    {
+        const int lo = tb_window_lo(a.groups[g].s_hi - first, n, m);
+        if (x < lo || x >= lo + kTbK)
+        {
+            a.tb_flag[p] = 1;
+            return;
+        }
+        a.gent[g] = x;
+        x = a.gtbl[(int64_t)g * kTbK + x - lo];
+        if (x < 0)
+        {
+            a.tb_flag[p] = 1;
+            return;
+        }
+    }
+    TbHead h;
+    h.kind = kRecRows;
+    h.tail_op = kLeft;
+    h.tail = x;  // row 0: LEFT to column 0 (traceBackNW :80-81)
+    h.nrec = m;
+    h.pad = 0;
+    h.score = a.pair_score[p];
+    h.i0 = m;
+    h.j0 = n;
+    h.start_text = 0;
+    h.start_pattern = 0;
+    a.heads[p] = h;
+    a.tb_flag[p] = 0;
+}
+
+// One block per group: thread 0 chains the group's strip tables from the group's entry column (each
+// strip's entry), then wave w walks strip s_hi - w from its entry with the row walk's staging and
+// unrolled batch, and writes its rows' records (record of row i at index m - i)
+__global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
+{
+    __shared__ int ent[kTbG];
+    const TbGroup g = a.groups[blockIdx.x];
+    if (uniform(a.tb_flag[uniform(g.pair)]) != 0) return;
+    const PairDesc pd = a.pairs[uniform(g.pair)];
+    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len), first = uniform(pd.first_strip);
+    const int sLo = uniform(g.s_lo), sHi = uniform(g.s_hi);
+    if (threadIdx.x == 0)
+    {
+        int x = a.gent[blockIdx.x];
+        for (int s = sHi; s >= sLo; --s)
+        {
+            ent[sHi - s] = x;
+            x = a.tbl[(int64_t)s * kTbK + x - tb_window_lo(s - first, n, m)];
+        }
+    }
+    __syncthreads();
+    const int w = uniform((int)(threadIdx.x / kWave)), lane = threadIdx.x & (kWave - 1);
+    const int s = sHi - w;
+    if (s < sLo) return;
+    const int b = s - first;
+    const int kTop = min(63, m - 1 - 64 * b);
+    const StripDesc sd = a.strips[s];
+    const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
+    int jo = uniform(ent[w]);
+    uint32_t W[8];
+    rw_stage<false>(sb, sb, INT_MIN, jo, lane, W);
+    Lines L;
+    L.kk = kTop;
+    auto restage = [&]() {
+        jo -= 16 * L.na;  // the eight windows are exhausted: the next 128 columns
+        L.na = 0;
+        L.u = 0;
+        rw_stage<false>(sb, sb, INT_MIN, jo, lane, W);
+    };
+    walk_batch<false>(L, a.fast != 0, 0, W, restage);
+    if (lane <= kTop) a.rec[uniform64(pd.rec_off) + (m - 1 - 64 * b - lane)] = (int32_t)L.vrec;
+}
+
+// ------------------------------------------------------------------------------------------------
 // expansion: records -> aligned strings (forward order) and the per-pair result
 // ------------------------------------------------------------------------------------------------
 // Grid (chunks, pairs): block c of a pair expands records [c * kChunkRecs, (c+1) * kChunkRecs), so a
@@ -1304,6 +1490,17 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
 {
     if (local) launch_walk_m<true>(R, a, np, st);
     else launch_walk_m<false>(R, a, np, st);
+}
+
+void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st)
+{
+    if (ngroups > 0)
+    {
+        hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
+    }
+    hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(kWave), 0, st, a);
+    if (ngroups > 0) hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
 }
 
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st)
