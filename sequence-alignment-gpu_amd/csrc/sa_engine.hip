@@ -317,11 +317,14 @@ struct sa_plan {
     Control *d_ctrl = nullptr;
     int32_t *d_rec = nullptr;  // traceback records (sa_walk.h)
     TbHead *d_heads = nullptr;
-    // table traceback (sa_walk.h TbArgs; R = 1 global plans with a pair of kTbMinStrips strips or more)
+    // table traceback (sa_walk.h TbArgs; R = 1 plans with a pair of kTbMinStrips strips or more)
     std::vector<TbGroup> tb_groups;
     std::vector<int32_t> tb_pg;  // [np + 1] first group of each pair
     TbGroup *d_tbgroups = nullptr;
-    int32_t *d_tbpg = nullptr, *d_tbl = nullptr, *d_gtbl = nullptr, *d_gent = nullptr, *d_tbflag = nullptr;
+    int32_t *d_tbpg = nullptr, *d_tbl = nullptr, *d_gtbl = nullptr, *d_gent = nullptr, *d_tbflag = nullptr, *d_win = nullptr;
+    int32_t *d_tbstart = nullptr, *d_sent = nullptr, *d_sdelta = nullptr, *d_send = nullptr, *d_pend = nullptr;
+    int64_t *d_csum = nullptr;  // expansion: per-chunk sums (pairs of more than kChunkRecs records)
+    int64_t max_recs = 1;       // records per pair at most (row walk: pattern rows, column walk: text columns)
     char *d_out_text = nullptr, *d_out_pattern = nullptr;
     sa_result *d_results = nullptr;
     const int8_t *d_text_in = nullptr, *d_pattern_in = nullptr;
@@ -397,7 +400,8 @@ void free_plan(sa_plan *p)
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
                     p->d_out_pattern, p->d_results, p->d_bands, p->d_tbgroups, p->d_tbpg, p->d_tbl,
-                    p->d_gtbl, p->d_gent, p->d_tbflag};
+                    p->d_gtbl, p->d_gent, p->d_tbflag, p->d_csum, p->d_win, p->d_tbstart, p->d_sent,
+                    p->d_sdelta, p->d_send, p->d_pend};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -845,7 +849,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         }
 
     // ---- table traceback groups (sa_walk.h) ----
-    if (pl->R == 1 && P->mode == SA_GLOBAL && knobs().tb_tables)
+    if (pl->R == 1 && knobs().tb_tables)
     {
         pl->tb_pg.assign(np + 1, 0);
         for (int64_t p = 0; p < np; ++p)
@@ -860,6 +864,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         if (pl->tb_groups.empty()) pl->tb_pg.clear();
     }
     const size_t ntg = pl->tb_groups.size();
+    for (const PairDesc &d : pl->pairs)
+        pl->max_recs = std::max<int64_t>(pl->max_recs, (int64_t)(pl->R == 1 ? d.pattern_len : d.text_len));
 
     // ---- device buffers ----
     const size_t nstr = std::max<size_t>(1, pl->strips.size()), npp = std::max<size_t>(1, np);
@@ -894,6 +900,13 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_gtbl, sizeof(int32_t) * kTbK * ntg},
         {(void **)&pl->d_gent, sizeof(int32_t) * ntg},
         {(void **)&pl->d_tbflag, ntg ? sizeof(int32_t) * npp : 0},
+        {(void **)&pl->d_win, ntg ? sizeof(int32_t) * nstr : 0},
+        {(void **)&pl->d_tbstart, ntg ? sizeof(int32_t) * 4 * npp : 0},
+        {(void **)&pl->d_pend, ntg ? sizeof(int32_t) * npp : 0},
+        {(void **)&pl->d_sent, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * nstr : 0},
+        {(void **)&pl->d_sdelta, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * nstr : 0},
+        {(void **)&pl->d_send, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * 4 * nstr : 0},
+        {(void **)&pl->d_csum, pl->max_recs > kChunkRecs ? sizeof(int64_t) * kMaxChunks * npp : 0},
     };
     int rc = SA_OK;
     if (ws)
@@ -1160,7 +1173,21 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         t.groups = pl->d_tbgroups;
         t.pair_g0 = pl->d_tbpg;
         t.pair_score = pl->d_score;
+        t.strip_best = pl->d_best;
+        t.start = pl->d_tbstart;
+        t.sent = pl->d_sent;
+        t.sdelta = pl->d_sdelta;
+        t.send = pl->d_send;
+        t.pend = pl->d_pend;
+        t.text = pl->d_text_in;
+        t.pattern = pl->d_pattern_in;
+        t.score_tab = pl->d_table;
+        t.A = pl->A;
+        t.gap = pl->gap;
+        t.key_rowbits = pl->key_rowbits;
+        t.local = pl->mode == SA_LOCAL ? 1 : 0;
         t.tbl = pl->d_tbl;
+        t.win = pl->d_win;
         t.gtbl = pl->d_gtbl;
         t.gent = pl->d_gent;
         t.tb_flag = pl->d_tbflag;
@@ -1187,11 +1214,9 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     x.ctrl = pl->d_ctrl;
     x.A = pl->A;
     std::memcpy(x.alphabet, pl->alphabet, 33);
+    x.chunk_sums = pl->d_csum;
     // records per pair: one per row (row walk, R = 1) or per column (column walk)
-    int64_t maxRecs = 1;
-    for (const PairDesc &d : pl->pairs)
-        maxRecs = std::max<int64_t>(maxRecs, (int64_t)(pl->R == 1 ? d.pattern_len : d.text_len));
-    launch_expand(x, np, maxRecs, st);
+    launch_expand(x, np, pl->max_recs, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "expand_kernel")) return rc;
     if (tmPath)

@@ -51,14 +51,18 @@ struct WalkArgs {
     const int32_t *tb_flag;        // null: every pair
 };
 
-// TABLE TRACEBACK (R = 1 global plans; sa_walk.hip tb_*_kernel). The sequential walk of a long pair
-// costs ~60 clk per row on one wave. Instead every strip b gets a TABLE: for each start column c of
-// a window of kTbK columns (tb_window_lo) the column at which the walk entering the strip's last row
-// at c enters the row above the strip (one lane per start column, all strips at once). Groups of kTbG
-// strips compose their tables; one wave per pair chains the group tables from (m, n) upward, which
-// gives every group's entry column, and each group then chains its strips' tables and walks its
-// strips in parallel (one wave each, the row walk's code), writing the records by row. A start
-// column outside a window ends the chain: the pair falls back to walk_rw_kernel (tb_flag).
+// TABLE TRACEBACK (R = 1 plans; sa_walk.hip tb_*_kernel). The sequential walk of a long pair costs
+// ~60 clk per row on one wave. Instead every strip b gets a TABLE: for each start column c of a window
+// of kTbK columns (tb_window_lo) the column at which the walk entering the strip's last row (the start
+// row in the start cell's strip) at c enters the row above the strip (all strips at once, the chains
+// that meet merged). Groups of kTbG strips compose their tables; one block per pair chains the group
+// tables from the start cell upward, which gives every group's entry column, and each group then
+// chains its strips' tables and walks its strips in parallel (one wave each, the row walk's code),
+// writing the records by row. A start column outside a window ends the chain: the pair falls back to
+// walk_rw_kernel (tb_flag). Local: the walk runs on the raw decisions (the R = 1 planes hold no
+// STOP) from the best cell down to row 1; each strip then sums its H steps, and tb_check_kernel finds
+// per strip, from H at the strip's entry (the sums of the strips before it), where traceBackSW ends
+// in it; the first such strip in walk order gives the pair's head (tb_finish_kernel).
 constexpr int kTbK = 2048;       // start columns per strip window
 constexpr int kTbG = 16;         // strips per group
 constexpr int kTbMinStrips = 8;  // pairs with fewer strips take the sequential walk
@@ -72,21 +76,32 @@ struct TbArgs {
     const TbGroup *groups;
     const int32_t *pair_g0;  // [np + 1]: pair p's groups are pair_g0[p] .. pair_g0[p + 1] - 1
     const int32_t *pair_score;
+    const uint64_t *strip_best;  // local: best-cell key per strip
+    int32_t *start;          // [pair][4] start cell i, j, its H, its strip (tb_start_kernel)
     int32_t *tbl;            // [strip][kTbK] exit column (-1: start column past n)
+    int32_t *win;            // [strip] first column of the strip's window (tb_table_kernel)
     int32_t *gtbl;           // [group][kTbK] exit column of the group (-1: left a window)
     int32_t *gent;           // [group] entry column (tb_resolve_kernel)
     int32_t *tb_flag;        // [pair] 1: walk_rw_kernel walks the pair
     int32_t *rec;
     TbHead *heads;
-    int32_t fast;
+    // local
+    int32_t *sent;           // [strip] entry column of the strip's first walked row (tb_walk_kernel)
+    int32_t *sdelta;         // [strip] H change over the strip's walked rows (tb_walk_kernel)
+    int32_t *send;           // [strip][4] where the walk ends in the strip: nrec, tail, start text / pattern
+    int32_t *pend;           // [pair] the strip of the end (highest strip with an end; tb_check_kernel)
+    const int8_t *text, *pattern;
+    const int32_t *score_tab;  // A x A, S + g (the plan's local table)
+    int32_t A, gap, key_rowbits, local, fast;
 };
 
-// First column of strip b's window (pair of n columns, m rows): kTbK columns centred on the diagonal
-// through (m, n) at the strip's last row (host and device)
-__host__ __device__ inline int tb_window_lo(int b, int n, int m)
+// First column of strip b's window: kTbK columns centred, at the strip's first walked row r, on the
+// diagonal through (m, n) and (0, 0) (global) or on the slope-1 line through the start cell (i0, j0)
+// (local), clamped to the pair's columns
+__host__ __device__ inline int tb_window_lo(int b, int n, int m, int i0, int j0, bool local)
 {
-    const int64_t r = b * 64 + 64 < m ? b * 64 + 64 : m;
-    const int64_t c = (r * n + m / 2) / m - kTbK / 2;
+    const int64_t r = b * 64 + 64 < i0 ? b * 64 + 64 : i0;
+    const int64_t c = (local ? (int64_t)j0 - (i0 - r) : (r * n + m / 2) / m) - kTbK / 2;
     const int64_t hi = n + 1 - kTbK > 0 ? n + 1 - kTbK : 0;
     return (int)(c < 0 ? 0 : (c > hi ? hi : c));
 }
@@ -102,6 +117,7 @@ struct ExpandArgs {
     const Control *ctrl;  // the plan's control word: a fill abort or bad input becomes every pair's status
     int32_t A;
     int32_t chunk_recs;  // records per expansion block (launch_expand sets it)
+    int64_t *chunk_sums; // [pair][kMaxChunks] packed op / letter counts per block (pairs of several blocks)
     char alphabet[33];
 };
 
@@ -109,8 +125,10 @@ struct ExpandArgs {
 void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st);
 // every plan: records -> aligned strings and sa_result; max_records bounds h.nrec over the pairs
 // (pattern rows for the row walk, text columns for the column walk)
-constexpr int kChunkRecs = 2048;  // records per expansion block (at least)
-constexpr int kMaxChunks = 64;    // blocks per pair (chunks past a pair's records exit at once)
+constexpr int kChunkRecs = 2048;    // pairs of at most this many records: one expansion block each
+constexpr int kMinChunkRecs = 256;  // records per block of a longer pair (at least)
+constexpr int kMaxChunks = 256;     // blocks per pair (chunks past a pair's records exit at once)
+// chunk_sums must hold np * kMaxChunks entries when max_records > kChunkRecs
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st);
 
 }  // namespace sa

@@ -499,6 +499,52 @@ __device__ void rw_stager(const WalkArgs &a, const uint32_t *mb, int64_t sstride
     }
 }
 
+// Where traceBackSW ends in a strip of the local row walk (the rows 64 cb + 1 .. 64 cb + ck + 1, lane l
+// = row 64 cb + l + 1, walked from lane ck down; per lane: H at the row's entry He, the row's record
+// run / dg, its entry column ce and leaving column lv = ce - run), if it does: the first row in walk
+// order where a cell's H is 0 (a STOP, alignSequenceCPU.cpp:18, :189) or a move goes onto row 0 /
+// column 0 (:44-46), and the head fields: records (cn0 before the strip), the trailing LEFT run, the
+// start indices (Response::startInAlignedText / Pattern). Uniform result.
+__device__ __forceinline__ bool local_strip_end(int He, int run, int dg, int ce, int lv, int cb, int ck, int cn0, int gap,
+                                                int lane, int &nrec, int &tail, int &st, int &sp0)
+{
+    const int row = 64 * cb + lane + 1;
+    int rz = INT_MAX;  // the first cell r = 0 .. run of the row whose H = He + g r is 0
+    if (He == 0) rz = 0;
+    else if (gap < 0 && He % (-gap) == 0) rz = He / (-gap);
+    const bool e1 = rz <= run && rz < ce;                       // STOP before column 0
+    const bool e2 = !e1 && lv <= 0;                              // the LEFT run reaches column 0
+    const bool e3 = !e1 && !e2 && (row == 1 || (dg && lv == 1)); // TOP / DIAG onto row 0 / column 0
+    const uint64_t ev = ballot(lane <= ck && (e1 || e2 || e3));
+    if (ev == 0) return false;
+    const int l = 63 - (int)__builtin_clzll(ev);  // the first in walk order (lane k down)
+    const int lrow = 64 * cb + l + 1;
+    const int lce = __builtin_amdgcn_readlane(ce, l), llv = __builtin_amdgcn_readlane(lv, l);
+    const int lrz = __builtin_amdgcn_readlane(rz, l), lrun = __builtin_amdgcn_readlane(run, l);
+    const bool l1 = (ballot(e1) >> l) & 1, l2 = (ballot(e2) >> l) & 1;
+    nrec = cn0 + (ck - l);
+    if (l1)
+    {
+        tail = lrz;  // the STOP cell (lrow, lce - lrz): every move into it updated the indices
+        st = lce - lrz - 1;
+        sp0 = lrow - 1;
+    }
+    else if (l2)
+    {
+        tail = lrun;  // LEFT moves to column 1, then onto column 0 without an index update
+        st = 0;
+        sp0 = lrow - 1;
+    }
+    else
+    {
+        nrec += 1;  // the row's record is whole; its move lands on the border (no index update)
+        tail = 0;
+        st = lrow == 1 ? llv - 1 : 0;
+        sp0 = lrow == 1 ? 0 : lrow - 1;
+    }
+    return true;
+}
+
 // Local row walk: the stager also runs local_check on every strip the walker posts. The walk runs on
 // the global encoding (the R = 1 planes hold no STOP), so where traceBackSW ends -- the first cell
 // whose H is 0 (a STOP, alignSequenceCPU.cpp:18, :189) or the first move onto row 0 / column 0
@@ -544,44 +590,12 @@ __device__ void rw_stager_local(const WalkArgs &a, const PairDesc &sp, const uin
             const int Pd = wave_prefix_sum(delta);
             const int tot = __builtin_amdgcn_readlane(Pd, ck);
             const int He = Hc + (tot - Pd);  // H at this lane's row entry
-            const int row = 64 * cb + lane + 1;
-            int rz = INT_MAX;  // the first cell r = 0 .. run of the row whose H = He + g r is 0
-            if (He == 0) rz = 0;
-            else if (a.gap < 0 && He % (-a.gap) == 0) rz = He / (-a.gap);
-            const bool e1 = rz <= run && rz < ce;                       // STOP before column 0
-            const bool e2 = !e1 && lv <= 0;                              // the LEFT run reaches column 0
-            const bool e3 = !e1 && !e2 && (row == 1 || (dg && lv == 1)); // TOP / DIAG onto row 0 / column 0
-            const uint64_t ev = ballot(lane <= ck && (e1 || e2 || e3));
-            if (ev == 0)
+            int nrec, tail, st, sp0;
+            if (!local_strip_end(He, run, dg, ce, lv, cb, ck, cn0, a.gap, lane, nrec, tail, st, sp0))
             {
                 Hc += tot;
                 if (lane == 0) ctl[2] = cseen;
                 continue;
-            }
-            const int l = 63 - (int)__builtin_clzll(ev);  // the first in walk order (lane k down)
-            const int lrow = 64 * cb + l + 1;
-            const int lce = __builtin_amdgcn_readlane(ce, l), llv = __builtin_amdgcn_readlane(lv, l);
-            const int lrz = __builtin_amdgcn_readlane(rz, l), lrun = __builtin_amdgcn_readlane(run, l);
-            const bool l1 = (ballot(e1) >> l) & 1, l2 = (ballot(e2) >> l) & 1;
-            int nrec = cn0 + (ck - l), tail, st, sp0;
-            if (l1)
-            {
-                tail = lrz;  // the STOP cell (lrow, lce - lrz): every move into it updated the indices
-                st = lce - lrz - 1;
-                sp0 = lrow - 1;
-            }
-            else if (l2)
-            {
-                tail = lrun;  // LEFT moves to column 1, then onto column 0 without an index update
-                st = 0;
-                sp0 = lrow - 1;
-            }
-            else
-            {
-                nrec += 1;  // the row's record is whole; its move lands on the border (no index update)
-                tail = 0;
-                st = lrow == 1 ? llv - 1 : 0;
-                sp0 = lrow == 1 ? 0 : lrow - 1;
             }
             if (lane == 0)
             {
@@ -1063,29 +1077,25 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 // ------------------------------------------------------------------------------------------------
 // table traceback (R = 1 global; sa_walk.h TbArgs)
 // ------------------------------------------------------------------------------------------------
-constexpr int kTbMargin = 320;                            // columns staged left of a window
-constexpr int kTbChunks = (kTbK + 63 + kTbMargin) / 32 + 2;  // R = 1 chunks staged per strip
-constexpr int kTbStride = kChunkDw + 4;                   // LDS dwords per chunk (padded: chunks on other banks)
+constexpr int kTbMargin = 320;                               // columns staged left of a window
+constexpr int kTbChunks = (kTbK + 63 + kTbMargin) / 32 + 2;  // R = 1 chunks (32 slots) staged per strip
+constexpr int kTbRow = kTbChunks + 1;                        // LDS dwords per strip row and mask
 
-// Word of strip lane k holding slot e (R = 1 interleaved planes, sa_layout.h): the staged copy when it
-// holds the chunk, else global memory
-__device__ __forceinline__ uint32_t tb_word(const uint32_t *buf, int clo, int nch, const uint32_t *sb, int k, int e)
-{
-    const int c = e >> 5, off = k * 2 + ((e >> 4) & 1);
-    return (unsigned)(c - clo) < (unsigned)nch ? buf[(c - clo) * kTbStride + off] : sb[(int64_t)c * kChunkDw + off];
-}
+typedef __attribute__((address_space(3))) const uint32_t tb_lds_u32;
+typedef __attribute__((address_space(1))) const uint32_t tb_glb_u32;
 
-// One row of traceBackNW (alignSequenceCPU.cpp:64-114) from entry column j of strip lane k: LEFT while
-// the cell is LEFT, then TOP or DIAG out of the row; column 0 is TOP (:78-79). Slot s of a word sits
+// One row of traceBackNW (alignSequenceCPU.cpp:64-114) from entry column j of strip lane k, word by
+// word from the raw planes in global memory (the rare lanes the staged probe leaves): LEFT while the
+// cell is LEFT, then TOP or DIAG out of the row; column 0 is TOP (:78-79). Slot s of a raw word sits
 // at bits 31 - 2s (plane 0, DIAG) and 30 - 2s (plane 1, up > left): the cell is not LEFT where either
 // is set, and the nearest such cell at or left of column j is the lowest set bit at or above 30 - 2s.
 // Returns the entry column of the row above.
-__device__ __forceinline__ int tb_row(int j, int k, const uint32_t *buf, int clo, int nch, const uint32_t *sb)
+__device__ __noinline__ int tb_row_slow(int j, int k, tb_glb_u32 *sb)
 {
     while (j > 0)
     {
-        const int e = j - 1 + k;
-        const uint32_t x = tb_word(buf, clo, nch, sb, k, e);
+        const int e = j - 1 + k;  // R = 1 slot of column j in strip lane k (sa_layout.h)
+        const uint32_t x = sb[(int64_t)(e >> 5) * kChunkDw + k * 2 + ((e >> 4) & 1)];
         const int s = e & 15;
         const uint32_t y = (x | (x >> 1)) & 0x55555555u & (0xffffffffu << (30 - 2 * s));
         if (y)
@@ -1098,128 +1108,299 @@ __device__ __forceinline__ int tb_row(int j, int k, const uint32_t *buf, int clo
     return 0;
 }
 
-// Strip tables: block = one strip, 1024 threads x 2 start columns (the window), the strip's planes
-// around the window staged in LDS; rows from the strip's last down to its first
+// 16 slots of a raw word -> 16 bits, slot s at bit s: the even bits 30 - 2s of y
+__device__ __forceinline__ uint32_t tb_slots16(uint32_t y)
+{
+    y &= 0x55555555u;
+    y = (y | (y >> 1)) & 0x33333333u;
+    y = (y | (y >> 2)) & 0x0F0F0F0Fu;
+    y = (y | (y >> 4)) & 0x00FF00FFu;
+    y = (y | (y >> 8)) & 0x0000FFFFu;
+    return __builtin_bitreverse32(y) >> 16;
+}
+
+// One row for a chain at column x (0: column 0, which stays there) from the staged masks: nl / dg
+// hold per strip row one bit per slot (slot e at bit e % 32 of dword e / 32 - clo; not LEFT / DIAG).
+// Two dwords cover the 33 .. 64 slots at and left of the entry; a longer LEFT run, or a slot outside the
+// staged chunks, goes through tb_row_slow.
+__device__ __forceinline__ int tb_step(int x, int k, tb_lds_u32 *nl, tb_lds_u32 *dg, int clo, int nch, tb_glb_u32 *gb)
+{
+    const int e = x - 1 + k, i = (e >> 5) - clo, bit = e & 31;
+    const bool in = x > 0 && (unsigned)i < (unsigned)nch && (i >= 1 || clo == 0);
+    const int ih = in ? k * kTbRow + i : 0, il = in && i >= 1 ? ih - 1 : ih;
+    const uint32_t nh = nl[ih] & (0xffffffffu >> (31 - bit)), dh = dg[ih];
+    const uint32_t nlo = i >= 1 ? nl[il] : 0u, dlo = dg[il];
+    const int ph = nh ? 31 - __builtin_clz(nh) : 0, pl = nlo ? 31 - __builtin_clz(nlo) : 0;
+    const int slot = nh ? e - bit + ph : (nlo ? e - bit - 32 + pl : INT_MIN);
+    const int d = nh ? (int)((dh >> ph) & 1u) : (int)((dlo >> pl) & 1u);
+    const int col = slot + 1 - k;
+    // nothing found: column 0 when the two words reach it (slot k - 1), else the slow walk
+    const int low = e - bit - (i >= 1 ? 32 : 0);
+    int r = slot != INT_MIN ? (col <= 0 ? 0 : col - d) : (low <= k ? 0 : -1);
+    if (!in) r = x > 0 ? -1 : 0;
+    return r >= 0 ? r : tb_row_slow(x, k, gb);
+}
+
+// Compaction of the distinct chains (tb_table_kernel): chains that met stay equal, and each run of
+// equal values in cur[0 .. D) becomes one chain (values of different runs may repeat: they stay apart,
+// which costs work, not correctness); map[] (start column -> chain) follows. Returns the new D.
+__device__ __forceinline__ int tb_compact(int *cur, uint16_t *map, uint16_t *tmp, int *wsum, int D)
+{
+    const int t = threadIdx.x, i0 = 2 * t, i1 = 2 * t + 1;
+    const int v0 = i0 < D ? cur[i0] : 0, v1 = i1 < D ? cur[i1] : 0;
+    const int vp = i0 > 0 && i0 < D ? cur[i0 - 1] : 0;
+    const int f0 = i0 < D && (i0 == 0 || v0 != vp), f1 = i1 < D && v1 != v0;
+    const int f = f0 + f1;
+    const int inc = wave_prefix_sum(f);
+    const int wv = t / kWave;
+    if ((t & (kWave - 1)) == kWave - 1) wsum[wv] = inc;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int k = 0; k < (int)(blockDim.x / kWave); ++k)
+    {
+        const int x = wsum[k];
+        before += k < wv ? x : 0;
+        total += x;
+    }
+    const int n0 = before + inc - f + f0 - 1, n1 = n0 + f1;  // new chain of elements i0, i1
+    if (i0 < D) tmp[i0] = (uint16_t)n0;
+    if (i1 < D) tmp[i1] = (uint16_t)n1;
+    __syncthreads();  // (every read of cur and wsum is done)
+    if (f0) cur[n0] = v0;
+    if (f1) cur[n1] = v1;
+    for (int c = t; c < kTbK; c += blockDim.x) map[c] = tmp[map[c]];
+    __syncthreads();
+    return total;
+}
+
+// Strip tables: block = one strip, 1024 threads, the kTbK start columns of the strip's window; the
+// strip's planes around the window staged in LDS as per-row masks (not LEFT, DIAG); rows from the
+// strip's last down to its first. Chains that meet stay merged, so after 4 and after 16 rows the
+// distinct ones are compacted (2048 -> ~500 -> ~230 at 32768^2 random DNA) and only those walk on.
+constexpr int kTbPhases = 3;
 __global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
 {
-    __shared__ uint32_t buf[kTbChunks * kTbStride];
+    __shared__ uint32_t nlm[kWave * kTbRow], dgm[kWave * kTbRow];
+    __shared__ int cur[kTbK];
+    __shared__ uint16_t map[kTbK], tmp[kTbK];
+    __shared__ int wsum[16];
     const int s = blockIdx.x;
     const StripDesc sd = a.strips[s];
     const int p = uniform(sd.pair);
-    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p])) return;  // (a pair of the sequential walk)
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 0) return;  // (sequential walk)
     const PairDesc pd = a.pairs[p];
     const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
+    const int i0 = uniform(a.start[4 * p]), j0 = uniform(a.start[4 * p + 1]), bs = uniform(a.start[4 * p + 3]);
     const int b = s - uniform(pd.first_strip);
-    const int kTop = min(63, m - 1 - 64 * b);
-    const int lo = tb_window_lo(b, n, m);
+    if (b > bs) return;  // (below the start cell)
+    const int kTop = b == bs ? (i0 - 1) & 63 : 63;
+    const int lo = tb_window_lo(b, n, m, i0, j0, a.local != 0);
+    if (threadIdx.x == 0) a.win[s] = lo;
     const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
     const int clo = max(0, (lo - 1 - kTbMargin) >> 5);
     const int nch = max(0, min(kTbChunks, (uniform(sd.nsteps) >> 5) - clo));
-    for (int e = threadIdx.x; e < nch * (kChunkDw / 4); e += blockDim.x)
+    for (int e = threadIdx.x; e < nch * kWave; e += blockDim.x)
     {
-        const int q = e / (kChunkDw / 4), r = e % (kChunkDw / 4);
-        *reinterpret_cast<uint4 *>(&buf[q * kTbStride + 4 * r]) =
-            *reinterpret_cast<const uint4 *>(sb + ((int64_t)clo + q) * kChunkDw + 4 * r);
+        const int q = e / kWave, k = e % kWave;  // chunk, strip lane: its two raw words (slots 0-15, 16-31)
+        const u32x2 v = *reinterpret_cast<const u32x2 *>(sb + ((int64_t)clo + q) * kChunkDw + 2 * k);
+        nlm[k * kTbRow + q] = tb_slots16(v.x | (v.x >> 1)) | (tb_slots16(v.y | (v.y >> 1)) << 16);
+        dgm[k * kTbRow + q] = tb_slots16(v.x >> 1) | (tb_slots16(v.y >> 1) << 16);
+    }
+    for (int t = threadIdx.x; t < kTbK; t += blockDim.x)
+    {
+        cur[t] = lo + t <= n ? lo + t : 0;  // (start columns past n: any chain, masked at the end)
+        map[t] = (uint16_t)t;
     }
     __syncthreads();
-    const int c0 = lo + (int)threadIdx.x, c1 = c0 + 1024;
-    int x0 = c0 <= n ? c0 : 0, x1 = c1 <= n ? c1 : 0;
-    for (int k = kTop; k >= 0; --k)
+    tb_lds_u32 *nl = (tb_lds_u32 *)nlm;
+    tb_lds_u32 *dg = (tb_lds_u32 *)dgm;
+    tb_glb_u32 *gb = (tb_glb_u32 *)sb;
+    constexpr int kRowsBefore[kTbPhases] = {4, 16, 64};  // rows walked before each compaction
+    int D = kTbK, k = kTop;
+    for (int ph = 0; ph < kTbPhases; ++ph)
     {
-        x0 = tb_row(x0, k, buf, clo, nch, sb);
-        x1 = tb_row(x1, k, buf, clo, nch, sb);
+        const int kEnd = max(-1, kTop - kRowsBefore[ph]);
+        for (int t = threadIdx.x; t < D; t += blockDim.x)
+        {
+            int x = cur[t];
+            for (int kk = k; kk > kEnd; --kk) x = tb_step(x, kk, nl, dg, clo, nch, gb);
+            cur[t] = x;
+        }
+        k = kEnd;
+        __syncthreads();
+        if (k < 0) break;
+        D = tb_compact(cur, map, tmp, wsum, D);
     }
     int32_t *out = a.tbl + (int64_t)s * kTbK;
-    out[threadIdx.x] = c0 <= n ? x0 : -1;
-    out[threadIdx.x + 1024] = c1 <= n ? x1 : -1;
+    for (int t = threadIdx.x; t < kTbK; t += blockDim.x) out[t] = lo + t <= n ? cur[map[t]] : -1;
 }
 
-// Group tables: the strip tables of the group chained from its last strip to its first, per start
-// column of the last strip's window (-1 once a column leaves a window)
+// Copies tables t0 .. t0 + nt - 1 (kTbK int32 each) of src into LDS (all threads of the block)
+__device__ __forceinline__ void tb_stage_tables(int32_t *dst, const int32_t *src, int64_t t0, int nt)
+{
+    const int4 *s4 = reinterpret_cast<const int4 *>(src + t0 * kTbK);
+    int4 *d4 = reinterpret_cast<int4 *>(dst);
+    for (int e = threadIdx.x; e < nt * (kTbK / 4); e += blockDim.x) d4[e] = s4[e];
+}
+
+// One wave per pair: the start cell (global: (m, n); local: the best cell, from the strips' keys as
+// walk_start), the strip holding it; tb_flag = 1 for the pairs of the sequential walk (no groups, or a
+// local pair without a positive cell: its empty alignment)
+__global__ __launch_bounds__(kWave) void tb_start_kernel(TbArgs a)
+{
+    const int p = blockIdx.x, lane = threadIdx.x;
+    const int g0 = uniform(a.pair_g0[p]), g1 = uniform(a.pair_g0[p + 1]);
+    const PairDesc pd = a.pairs[p];
+    int i = (int)pd.pattern_len, j = (int)pd.text_len, H = 0;
+    bool ok = g1 > g0;
+    if (ok && a.local)
+    {
+        const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
+        uint64_t k = 0;
+        for (int s = lane; s < nstrips; s += kWave) k = max(k, a.strip_best[first + s]);
+        k = wave_max_u64(k);
+        const int rb = a.key_rowbits;
+        const uint64_t km = (1ull << rb) - 1;
+        H = (int)(k >> (2 * rb));
+        i = (int)(km - ((k >> rb) & km));
+        j = (int)(km - (k & km));
+        ok = H > 0;
+    }
+    else if (ok)
+        H = a.pair_score[p];
+    if (lane != 0) return;
+    a.tb_flag[p] = ok ? 0 : 1;
+    if (!ok) return;
+    a.start[4 * p] = i;
+    a.start[4 * p + 1] = j;
+    a.start[4 * p + 2] = H;
+    a.start[4 * p + 3] = (i - 1) >> 6;
+    a.pend[p] = -1;
+}
+
+// The group's strips walked from the start: s_lo .. min(s_hi, the start cell's strip); false if none
+__device__ __forceinline__ bool tb_group_span(const TbArgs &a, const TbGroup &g, const PairDesc &pd, int &sLo, int &sHi)
+{
+    sLo = uniform(g.s_lo);
+    sHi = min(uniform(g.s_hi), uniform(pd.first_strip) + uniform(a.start[4 * uniform(g.pair) + 3]));
+    return sHi >= sLo;
+}
+
+// Group tables: the strip tables of the group (staged in LDS) chained from its first walked strip to
+// its last, per start column of the first strip's window (-1 once a column leaves a window)
 __global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
 {
+    __shared__ int32_t tl[kTbG * kTbK];
+    __shared__ int wl[kTbG];
     const TbGroup g = a.groups[blockIdx.x];
+    if (uniform(a.tb_flag[uniform(g.pair)]) != 0) return;
     const PairDesc pd = a.pairs[uniform(g.pair)];
-    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len), first = uniform(pd.first_strip);
-    const int sLo = uniform(g.s_lo), sHi = uniform(g.s_hi);
-    const int loHi = tb_window_lo(sHi - first, n, m);
+    int sLo, sHi;
+    if (!tb_group_span(a, g, pd, sLo, sHi)) return;
+    const int n = uniform((int)pd.text_len);
+    tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
+    if (threadIdx.x <= sHi - sLo) wl[threadIdx.x] = a.win[sLo + threadIdx.x];
+    __syncthreads();
+    const int loHi = wl[sHi - sLo];
     for (int t = threadIdx.x; t < kTbK; t += blockDim.x)
     {
         int x = loHi + t <= n ? loHi + t : -1;
         for (int s = sHi; s >= sLo && x >= 0; --s)
         {
-            const int lo = tb_window_lo(s - first, n, m);
-            x = (x >= lo && x < lo + kTbK) ? a.tbl[(int64_t)s * kTbK + x - lo] : -1;
+            const int lo = wl[s - sLo];
+            x = (x >= lo && x < lo + kTbK) ? tl[(s - sLo) * kTbK + x - lo] : -1;
         }
         a.gtbl[(int64_t)blockIdx.x * kTbK + t] = x;
     }
 }
 
-// One wave per pair: the group tables chained from (m, n) upward give every group's entry column and
-// the row-0 column (the trailing LEFT run); the pair's head. A column outside a window: tb_flag = 1
-// and walk_rw_kernel walks the pair instead.
-__global__ __launch_bounds__(64) void tb_resolve_kernel(TbArgs a)
+// One block per pair: the group tables chained from the start cell upward (staged in LDS kTbG at a
+// time) give every group's entry column and the row-0 column; global: the pair's head (the trailing
+// LEFT run). A column outside a window: tb_flag = 1 and walk_rw_kernel walks the pair instead.
+__global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
 {
+    __shared__ int32_t tl[kTbG * kTbK];
+    __shared__ int xs;
     const int p = blockIdx.x;
+    if (uniform(a.tb_flag[p]) != 0) return;
+    const int g0 = uniform(a.pair_g0[p]), g1 = uniform(a.pair_g0[p + 1]);
+    const PairDesc pd = a.pairs[p];
+    const int first = uniform(pd.first_strip), bs = uniform(a.start[4 * p + 3]);
+    // the groups walked: g0 .. gs (gs holds the start cell's strip)
+    int gs = g1 - 1;
+    while (gs > g0 && uniform(a.groups[gs].s_lo) > first + bs) --gs;
+    if (threadIdx.x == 0) xs = a.start[4 * p + 1];
+    for (int gh = gs + 1; gh > g0; gh -= kTbG)
+    {
+        const int gl = max(g0, gh - kTbG);
+        __syncthreads();  // (the previous chunk's lookups are done)
+        tb_stage_tables(tl, a.gtbl, gl, gh - gl);
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            int x = xs;
+            for (int g = gh - 1; g >= gl && x >= 0; --g)
+            {
+                const int lo = a.win[min(a.groups[g].s_hi, first + bs)];
+                if (x < lo || x >= lo + kTbK)
+                    x = -1;
+                else
+                {
+                    a.gent[g] = x;
+                    x = tl[(g - gl) * kTbK + x - lo];
+                }
+            }
+            xs = x;
+        }
+    }
+    __syncthreads();
     if (threadIdx.x != 0) return;
-    const int g0 = a.pair_g0[p], g1 = a.pair_g0[p + 1];
-    if (g1 == g0)
+    const int x = xs;
+    if (x < 0)
     {
         a.tb_flag[p] = 1;
         return;
     }
-    const PairDesc pd = a.pairs[p];
-    const int n = (int)pd.text_len, m = (int)pd.pattern_len, first = pd.first_strip;
-    int x = n;
-    for (int g = g1 - 1; g >= g0; --g)
-    {
-        const int lo = tb_window_lo(a.groups[g].s_hi - first, n, m);
-        if (x < lo || x >= lo + kTbK)
-        {
-            a.tb_flag[p] = 1;
-            return;
-        }
-        a.gent[g] = x;
-        x = a.gtbl[(int64_t)g * kTbK + x - lo];
-        if (x < 0)
-        {
-            a.tb_flag[p] = 1;
-            return;
-        }
-    }
+    if (a.local) return;  // (the head: tb_finish_kernel)
     TbHead h;
     h.kind = kRecRows;
     h.tail_op = kLeft;
     h.tail = x;  // row 0: LEFT to column 0 (traceBackNW :80-81)
-    h.nrec = m;
+    h.nrec = (int)pd.pattern_len;
     h.pad = 0;
-    h.score = a.pair_score[p];
-    h.i0 = m;
-    h.j0 = n;
+    h.score = a.start[4 * p + 2];
+    h.i0 = (int)pd.pattern_len;
+    h.j0 = (int)pd.text_len;
     h.start_text = 0;
     h.start_pattern = 0;
     a.heads[p] = h;
-    a.tb_flag[p] = 0;
 }
 
-// One block per group: thread 0 chains the group's strip tables from the group's entry column (each
-// strip's entry), then wave w walks strip s_hi - w from its entry with the row walk's staging and
-// unrolled batch, and writes its rows' records (record of row i at index m - i)
+// One block per group: thread 0 chains the group's strip tables (staged in LDS) from the group's entry
+// column (each strip's entry), then wave w walks strip sHi - w from its entry with the row walk's
+// staging and unrolled batch and writes its rows' records (record of row i at index i0 - i); local:
+// the strip's entry column and the sum of its H steps (local_check's, see rw_stager_local)
 __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
 {
+    __shared__ int32_t tl[kTbG * kTbK];
     __shared__ int ent[kTbG];
     const TbGroup g = a.groups[blockIdx.x];
-    if (uniform(a.tb_flag[uniform(g.pair)]) != 0) return;
-    const PairDesc pd = a.pairs[uniform(g.pair)];
-    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len), first = uniform(pd.first_strip);
-    const int sLo = uniform(g.s_lo), sHi = uniform(g.s_hi);
+    const int p = uniform(g.pair);
+    if (uniform(a.tb_flag[p]) != 0) return;
+    const PairDesc pd = a.pairs[p];
+    int sLo, sHi;
+    if (!tb_group_span(a, g, pd, sLo, sHi)) return;
+    const int first = uniform(pd.first_strip);
+    const int i0 = uniform(a.start[4 * p]), bs = uniform(a.start[4 * p + 3]);
+    tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
+    __syncthreads();
     if (threadIdx.x == 0)
     {
         int x = a.gent[blockIdx.x];
         for (int s = sHi; s >= sLo; --s)
         {
             ent[sHi - s] = x;
-            x = a.tbl[(int64_t)s * kTbK + x - tb_window_lo(s - first, n, m)];
+            x = tl[(s - sLo) * kTbK + x - a.win[s]];
         }
     }
     __syncthreads();
@@ -1227,10 +1408,11 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
     const int s = sHi - w;
     if (s < sLo) return;
     const int b = s - first;
-    const int kTop = min(63, m - 1 - 64 * b);
+    const int kTop = b == bs ? (i0 - 1) & 63 : 63;
     const StripDesc sd = a.strips[s];
     const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
-    int jo = uniform(ent[w]);
+    const int jc = uniform(ent[w]);
+    int jo = jc;
     uint32_t W[8];
     rw_stage<false>(sb, sb, INT_MIN, jo, lane, W);
     Lines L;
@@ -1242,18 +1424,103 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
         rw_stage<false>(sb, sb, INT_MIN, jo, lane, W);
     };
     walk_batch<false>(L, a.fast != 0, 0, W, restage);
-    if (lane <= kTop) a.rec[uniform64(pd.rec_off) + (m - 1 - 64 * b - lane)] = (int32_t)L.vrec;
+    if (lane <= kTop) a.rec[uniform64(pd.rec_off) + (i0 - 1 - 64 * b - lane)] = (int32_t)L.vrec;
+    if (!a.local) return;
+    // the strip's H steps: a row entered at H adds g per LEFT cell, its leaving TOP adds g, its leaving
+    // DIAG subtracts S of its cell (the letters gathered from the inputs)
+    const int pv = (int)L.vrec;
+    const int run = lane <= kTop ? pv >> 1 : 0, dg = lane <= kTop ? pv & 1 : 0;
+    const int P = wave_prefix_sum(run + dg);
+    const int ce = jc - (__builtin_amdgcn_readlane(P, kTop) - P), lv = ce - run;
+    const int pl = lane <= kTop ? (int)a.pattern[pd.pattern_off + 64 * b + lane] : 0;
+    const int tl2 = lane <= kTop && dg && lv >= 1 ? (int)a.text[pd.text_off + lv - 1] : 0;
+    const int S = dg ? a.score_tab[pl * a.A + tl2] - a.gap : 0;  // (the table holds S + g)
+    const int delta = lane <= kTop ? a.gap * run + (dg ? -S : a.gap) : 0;
+    const int tot = __builtin_amdgcn_readlane(wave_prefix_sum(delta), kWave - 1);
+    if (lane == 0)
+    {
+        a.sent[s] = jc;
+        a.sdelta[s] = tot;
+    }
+}
+
+// Local, one wave per strip walked: H at the strip's entry (the start cell's H plus the sums of the
+// strips walked before it), then local_strip_end on the strip's records (as rw_stager_local); a strip
+// where the walk ends writes its head fields and raises the pair's end strip to it
+__global__ __launch_bounds__(kWave) void tb_check_kernel(TbArgs a)
+{
+    const int s = blockIdx.x, lane = threadIdx.x;
+    const StripDesc sd = a.strips[s];
+    const int p = uniform(sd.pair);
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 0) return;
+    const PairDesc pd = a.pairs[p];
+    const int first = uniform(pd.first_strip);
+    const int i0 = uniform(a.start[4 * p]), bs = uniform(a.start[4 * p + 3]);
+    const int b = s - first;
+    if (b > bs) return;
+    int hsum = 0;
+    for (int q = b + 1 + lane; q <= bs; q += kWave) hsum += a.sdelta[first + q];
+    const int Hc = uniform(a.start[4 * p + 2]) + __builtin_amdgcn_readlane(wave_prefix_sum(hsum), kWave - 1);
+    const int kTop = b == bs ? (i0 - 1) & 63 : 63;
+    const int jc = uniform(a.sent[s]);
+    const int cn0 = i0 - (64 * b + kTop + 1);
+    const int pv = lane <= kTop ? a.rec[uniform64(pd.rec_off) + (i0 - 1 - 64 * b - lane)] : 0;
+    const int run = lane <= kTop ? pv >> 1 : 0, dg = lane <= kTop ? pv & 1 : 0;
+    const int P = wave_prefix_sum(run + dg);
+    const int ce = jc - (__builtin_amdgcn_readlane(P, kTop) - P), lv = ce - run;
+    const int pl = lane <= kTop ? (int)a.pattern[pd.pattern_off + 64 * b + lane] : 0;
+    const int tl2 = lane <= kTop && dg && lv >= 1 ? (int)a.text[pd.text_off + lv - 1] : 0;
+    const int S = dg ? a.score_tab[pl * a.A + tl2] - a.gap : 0;
+    const int delta = lane <= kTop ? a.gap * run + (dg ? -S : a.gap) : 0;
+    const int Pd = wave_prefix_sum(delta);
+    const int tot = __builtin_amdgcn_readlane(Pd, kTop);
+    const int He = Hc + (tot - Pd);  // H at this lane's row entry
+    int nrec, tail, st, sp0;
+    if (!local_strip_end(He, run, dg, ce, lv, b, kTop, cn0, a.gap, lane, nrec, tail, st, sp0)) return;
+    if (lane != 0) return;
+    a.send[4 * s] = nrec;
+    a.send[4 * s + 1] = tail;
+    a.send[4 * s + 2] = st;
+    a.send[4 * s + 3] = sp0;
+    atomicMax(&a.pend[p], b);
+}
+
+// Local, one thread per pair: the head from the end strip (the highest strip with an end: the first in
+// walk order); a pair without one (never: row 1 always ends the walk) goes to walk_rw_kernel
+__global__ __launch_bounds__(kWave) void tb_finish_kernel(TbArgs a)
+{
+    const int p = blockIdx.x;
+    if (threadIdx.x != 0 || a.pair_g0[p + 1] == a.pair_g0[p] || a.tb_flag[p] != 0) return;
+    const int b = a.pend[p];
+    if (b < 0)
+    {
+        a.tb_flag[p] = 1;
+        return;
+    }
+    const int s = a.pairs[p].first_strip + b;
+    TbHead h;
+    h.kind = kRecRows;
+    h.tail_op = kLeft;
+    h.nrec = a.send[4 * s];
+    h.tail = a.send[4 * s + 1];
+    h.start_text = a.send[4 * s + 2];
+    h.start_pattern = a.send[4 * s + 3];
+    h.pad = 0;
+    h.score = a.start[4 * p + 2];
+    h.i0 = a.start[4 * p];
+    h.j0 = a.start[4 * p + 1];
+    a.heads[p] = h;
 }
 
 // ------------------------------------------------------------------------------------------------
 // expansion: records -> aligned strings (forward order) and the per-pair result
 // ------------------------------------------------------------------------------------------------
-// Grid (chunks, pairs): block c of a pair expands records [c * kChunkRecs, (c+1) * kChunkRecs), so a
-// single long pair spreads over up to kMaxChunks CUs (one workgroup took 0.18 ms at 32768^2). A block
-// whose chunk is not the whole pair first sums every record of the pair (the total length L fixes the
-// forward positions) and those before its chunk (its starting position and letter counts) in one
-// strided pass — O(N) reads per block, served by L2; a block holding all of its pair's records (the
-// batch: one chunk per pair) takes the totals from its own scan. Each thread expands a run of
+// Grid (chunks, pairs): block c of a pair expands records [c * chunk_recs, (c+1) * chunk_recs), so a
+// single long pair spreads over up to kMaxChunks CUs (one workgroup took 0.18 ms at 32768^2). Pairs of
+// several chunks: expand_sum_kernel first writes each chunk's packed op / letter counts, and a block
+// sums those of its pair (the total length L fixes the forward positions) and of the chunks before it
+// (its starting position and letter counts); a block holding all of its pair's records (the batch: one
+// chunk per pair) takes the totals from its own scan. Each thread expands a run of
 // consecutive records; their letters go to an LDS copy of the chunk's slice of both strings when it
 // fits (kStage bytes each), which the block then writes out in aligned dwords (per-thread byte runs
 // land ~10 bytes apart, one uncoalesced byte store per letter), else straight to HBM. Block 0 also
@@ -1351,6 +1618,22 @@ __device__ __forceinline__ void expand_records(const TbHead &h, const int32_t *r
     }
 }
 
+// Per-chunk sums of rec_counts (pairs of several chunks)
+__global__ __launch_bounds__(kExpThreads) void expand_sum_kernel(ExpandArgs a)
+{
+    __shared__ int64_t scan[2 * kExpThreads];
+    const int p = blockIdx.y;
+    const int N = a.heads[p].nrec;
+    const int c0 = (int)blockIdx.x * a.chunk_recs;
+    if (N <= a.chunk_recs || c0 >= N) return;  // (uniform per block)
+    const int32_t *rec = a.rec + a.pairs[p].rec_off;
+    const int cend = min(N, c0 + a.chunk_recs);
+    int64_t x = 0, y = 0;
+    for (int q = c0 + (int)threadIdx.x; q < cend; q += kExpThreads) x += rec_counts(rec[q]);
+    block_sum2(x, y, scan);
+    if (threadIdx.x == 0) a.chunk_sums[(int64_t)p * kMaxChunks + blockIdx.x] = x;
+}
+
 __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
 {
     __shared__ int64_t scan[2 * kExpThreads];
@@ -1375,11 +1658,12 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
     int64_t tot = 0, pre = 0;
     if (!whole)
     {
-        for (int q = t; q < N; q += kExpThreads)
+        const int nch = (N + a.chunk_recs - 1) / a.chunk_recs;
+        for (int c = t; c < nch; c += kExpThreads)
         {
-            const int64_t x = rec_counts(rec[q]);
+            const int64_t x = a.chunk_sums[(int64_t)p * kMaxChunks + c];
             tot += x;
-            pre += q < c0 ? x : 0;
+            pre += c < (int)blockIdx.x ? x : 0;
         }
         block_sum2(tot, pre, scan);
     }
@@ -1494,22 +1778,26 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
 
 void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st)
 {
-    if (ngroups > 0)
+    hipLaunchKernelGGL(tb_start_kernel, dim3(np), dim3(kWave), 0, st, a);
+    hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
+    if (a.local)
     {
-        hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(1024), 0, st, a);
-        hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(tb_check_kernel, dim3(nstrips), dim3(kWave), 0, st, a);
+        hipLaunchKernelGGL(tb_finish_kernel, dim3(np), dim3(kWave), 0, st, a);
     }
-    hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(kWave), 0, st, a);
-    if (ngroups > 0) hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
 }
 
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st)
 {
     ExpandArgs x = a;
     const int64_t recs = std::max<int64_t>(1, max_records);
-    const int64_t per = std::max<int64_t>(kChunkRecs, (recs + kMaxChunks - 1) / kMaxChunks);
+    const int64_t per = recs <= kChunkRecs ? kChunkRecs : std::max<int64_t>(kMinChunkRecs, (recs + kMaxChunks - 1) / kMaxChunks);
     x.chunk_recs = (int)per;
     const int chunks = (int)((recs + per - 1) / per);
+    if (chunks > 1) hipLaunchKernelGGL(expand_sum_kernel, dim3(chunks, np), dim3(kExpThreads), 0, st, x);
     hipLaunchKernelGGL(expand_kernel, dim3(chunks, np), dim3(kExpThreads), 0, st, x);
 }
 

@@ -1,12 +1,14 @@
 """Table traceback (sa_walk.hip tb_*_kernel, sa_walk.h TbArgs): every strip's window of start columns
 is walked in parallel into a table, the tables are chained per group and per pair, and each group's
-strips are then walked in parallel from their now-known entry columns. Checked in subprocesses (the
-engine reads its knobs once per process) against the oracle's full alignment (traceBackNW,
-alignSequenceCPU.cpp:64-114):
+strips are then walked in parallel from their now-known entry columns (local: then where the walk
+ends, from H summed along the path). Checked in subprocesses (the engine reads its knobs once per
+process) against the oracle's full alignment in both modes (traceBackNW / traceBackSW,
+alignSequenceCPU.cpp:64-114 / :10-62):
   * SA_TB_STRICT=1 (no sequential walk afterwards): every pair below must be resolved by the tables
     alone, so a wrong or missing table result shows as a wrong alignment;
-  * default: a pair whose path leaves the windows (a long insertion far off the diagonal; unrelated
-    pairs of unequal lengths, cases 3 and 4) falls back to the sequential walk and is still exact;
+  * default: a pair whose path leaves the windows (a long insertion far off the diagonal; global
+    unrelated pairs of unequal lengths, cases 3 and 4; a local alignment across a 1500-column gap)
+    falls back to the sequential walk and is still exact;
   * SA_TB_TABLES=0: the sequential walk alone on the same pairs."""
 from __future__ import annotations
 
@@ -27,22 +29,28 @@ S = synthetic.blast_matrix()
 B50 = np.array(json.load(open(sys.argv[1] + "/tests/golden/matrices.json"))["blosum50"], np.int32).reshape(23, 23)
 which = sys.argv[2]
 bad = []
-def one(t, p, S, gap, tag):
-    r = engine.align_pair(0, t, p, S, gap, device=0)
+def one(t, p, S, gap, tag, mode=0):
+    r = engine.align_pair(mode, t, p, S, gap, device=0)
     r.pop("fill_us")
-    if r != oracle.align(0, t, p, S, gap):
-        bad.append(tag)
+    if r != oracle.align(mode, t, p, S, gap):
+        bad.append(tag + (mode,))
 cases = [  # (n, m, gap, related, alphabet) -- m rows (8+ strips), n columns
     (4096, 4096, 5, False, 4), (4096, 4096, 5, True, 4), (1000, 5000, 5, True, 4), (3000, 20000, 5, False, 4),
     (20000, 3000, 5, False, 4), (9000, 8191, 0, True, 4), (5000, 4097, -2, False, 4), (600, 700, 5, False, 4),
     (3000, 2000, 5, False, 23), (2500, 2600, 5, True, 23), (2047, 4000, 5, False, 4), (2049, 4000, 5, True, 4)]
 for k, (n, m, gap, rel, A) in enumerate(cases):
-    if which == "strict" and k in (3, 4):
-        continue  # unrelated pairs of unequal lengths: the path strays from the line through (m, n), (0, 0)
     t = synthetic.random_sequence(70 + k, n, 4 if A == 4 else 20)
     p = synthetic.mutate(t, 90 + k, 4 if A == 4 else 20, m) if rel else synthetic.random_sequence(110 + k, m, 4 if A == 4 else 20)
-    one(t, p, S if A == 4 else B50, gap, ("case", k))
+    for mode in (0, 1):
+        if which == "strict" and mode == 0 and k in (3, 4):
+            continue  # unrelated pairs of unequal lengths: the path strays from the line through (m, n), (0, 0)
+        one(t, p, S if A == 4 else B50, gap, ("case", k), mode)
 if which == "fallback":
+    # local: two copied segments of the text 1500 columns apart, one alignment across the gap (the
+    # path leaves the slope-1 line through the best cell by 1500 columns)
+    t = synthetic.random_sequence(210, 10000, 4)
+    p = np.concatenate([t[500:4000], t[5500:9000]])
+    one(t, p, S, 5, ("fallback_local", 0), 1)
     # the pattern matches the END of a much longer text: the path runs down the diagonal near column n
     # and then LEFT along row ~0, far from the line through (m, n) and (0, 0) (windows of 2048 columns)
     t = synthetic.random_sequence(200, 12000, 4)
@@ -51,10 +59,11 @@ if which == "fallback":
     # several pairs in one plan: table pairs, a fallback pair and short pairs (sequential walk)
     ts = [synthetic.random_sequence(300 + k, 900 + 1700 * k, 4) for k in range(4)] + [t]
     ps = [synthetic.mutate(ts[k], 310 + k, 4, 200 + 1300 * k) for k in range(4)] + [p]
-    got = engine.align_batch(0, ts, ps, S, 5, num_gpus=1)
-    for k in range(5):
-        if got[k] != oracle.align(0, ts[k], ps[k], S, 5):
-            bad.append(("batch", k))
+    for mode in (0, 1):
+        got = engine.align_batch(mode, ts, ps, S, 5, num_gpus=1)
+        for k in range(5):
+            if got[k] != oracle.align(mode, ts[k], ps[k], S, 5):
+                bad.append(("batch", k, mode))
 print("TB_OK" if not bad else "TB_BAD %r" % (bad,))
 '''
 
