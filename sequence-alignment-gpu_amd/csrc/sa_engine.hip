@@ -200,6 +200,7 @@ struct Knobs {
     int chain_lds_kb = 0;           // SA_CHAIN_LDS_KB: dynamic LDS per chain workgroup
     const char *timeline = nullptr; // SA_TIMELINE=<file>: per-strip fill timestamps
     const char *tb_timing = nullptr;// SA_TB_TIMING=<file>: per-pair traceback timestamps
+    const char *tb_table_timing = nullptr;  // SA_TB_TABLE_TIMING=<file>: per-strip table kernel stamps
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
     bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
     bool tb_tables = true;          // SA_TB_TABLES=0: no table traceback (every pair walks sequentially)
@@ -226,6 +227,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_CHAIN_LDS_KB")) v.chain_lds_kb = std::max(0, std::atoi(e));
         v.timeline = get("SA_TIMELINE");
         v.tb_timing = get("SA_TB_TIMING");
+        v.tb_table_timing = get("SA_TB_TABLE_TIMING");
         v.tb_generic = get("SA_TB_GENERIC") != nullptr;
         if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
         if (const char *e = get("SA_TB_TABLES")) v.tb_tables = std::atoi(e) != 0;
@@ -1186,6 +1188,15 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         t.gap = pl->gap;
         t.key_rowbits = pl->key_rowbits;
         t.local = pl->mode == SA_LOCAL ? 1 : 0;
+        t.dbg = nullptr;
+        DevPtr<uint64_t> dbgBuf;
+        const size_t dbgWords = 12 * pl->strips.size();
+        if (kn.tb_table_timing)
+        {
+            HIP_TRY(hipMalloc((void **)&t.dbg, sizeof(uint64_t) * dbgWords));
+            dbgBuf.reset(t.dbg);
+            HIP_TRY(hipMemsetAsync(t.dbg, 0, sizeof(uint64_t) * dbgWords, st));
+        }
         t.tbl = pl->d_tbl;
         t.win = pl->d_win;
         t.gtbl = pl->d_gtbl;
@@ -1196,6 +1207,17 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         t.fast = w.fast;
         launch_tb(t, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, st);
         HIP_TRY(hipGetLastError());
+        if (kn.tb_table_timing)
+        {
+            std::vector<uint64_t> v(dbgWords);
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(hipMemcpy(v.data(), t.dbg, v.size() * 8, hipMemcpyDeviceToHost));
+            if (FILE *f = std::fopen(kn.tb_table_timing, "wb"))
+            {
+                std::fwrite(v.data(), 8, v.size(), f);
+                std::fclose(f);
+            }
+        }
         if (int rc = debug_sync(st, "table traceback")) return rc;
         w.tb_flag = pl->d_tbflag;
     }

@@ -93,6 +93,7 @@ struct TbArgs {
     const int8_t *text, *pattern;
     const int32_t *score_tab;  // A x A, S + g (the plan's local table)
     int32_t A, gap, key_rowbits, local, fast;
+    uint64_t *dbg;             // debug (SA_TB_TABLE_TIMING): per strip 12 words of tb_table_kernel stamps
 };
 
 // First column of strip b's window: kTbK columns centred, at the strip's first walked row r, on the

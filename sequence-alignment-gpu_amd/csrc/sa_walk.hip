@@ -1079,34 +1079,10 @@ __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
 // ------------------------------------------------------------------------------------------------
 constexpr int kTbMargin = 320;                               // columns staged left of a window
 constexpr int kTbChunks = (kTbK + 63 + kTbMargin) / 32 + 2;  // R = 1 chunks (32 slots) staged per strip
-constexpr int kTbRow = kTbChunks + 1;                        // LDS dwords per strip row and mask
+constexpr int kTbRow = kTbChunks + 2;                        // LDS dwords per strip row and mask (a zero word first)
+constexpr int kTbNz = (kTbChunks + 31) / 32;                 // dwords of a row's nonzero-word mask
 
 typedef __attribute__((address_space(3))) const uint32_t tb_lds_u32;
-typedef __attribute__((address_space(1))) const uint32_t tb_glb_u32;
-
-// One row of traceBackNW (alignSequenceCPU.cpp:64-114) from entry column j of strip lane k, word by
-// word from the raw planes in global memory (the rare lanes the staged probe leaves): LEFT while the
-// cell is LEFT, then TOP or DIAG out of the row; column 0 is TOP (:78-79). Slot s of a raw word sits
-// at bits 31 - 2s (plane 0, DIAG) and 30 - 2s (plane 1, up > left): the cell is not LEFT where either
-// is set, and the nearest such cell at or left of column j is the lowest set bit at or above 30 - 2s.
-// Returns the entry column of the row above.
-__device__ __noinline__ int tb_row_slow(int j, int k, tb_glb_u32 *sb)
-{
-    while (j > 0)
-    {
-        const int e = j - 1 + k;  // R = 1 slot of column j in strip lane k (sa_layout.h)
-        const uint32_t x = sb[(int64_t)(e >> 5) * kChunkDw + k * 2 + ((e >> 4) & 1)];
-        const int s = e & 15;
-        const uint32_t y = (x | (x >> 1)) & 0x55555555u & (0xffffffffu << (30 - 2 * s));
-        if (y)
-        {
-            const int q = __builtin_ctz(y);
-            return j - (s - ((30 - q) >> 1)) - (int)((x >> (q + 1)) & 1u);
-        }
-        j -= s + 1;  // a LEFT run past this word
-    }
-    return 0;
-}
 
 // 16 slots of a raw word -> 16 bits, slot s at bit s: the even bits 30 - 2s of y
 __device__ __forceinline__ uint32_t tb_slots16(uint32_t y)
@@ -1119,38 +1095,76 @@ __device__ __forceinline__ uint32_t tb_slots16(uint32_t y)
     return __builtin_bitreverse32(y) >> 16;
 }
 
-// One row for a chain at column x (0: column 0, which stays there) from the staged masks: nl / dg
-// hold per strip row one bit per slot (slot e at bit e % 32 of dword e / 32 - clo; not LEFT / DIAG).
-// Two dwords cover the 33 .. 64 slots at and left of the entry; a longer LEFT run, or a slot outside the
-// staged chunks, goes through tb_row_slow.
-__device__ __forceinline__ int tb_step(int x, int k, tb_lds_u32 *nl, tb_lds_u32 *dg, int clo, int nch, tb_glb_u32 *gb)
+// One row of traceBackNW (alignSequenceCPU.cpp:64-114) for a chain entering strip row k at column
+// x >= 1: LEFT while the cell is LEFT, then TOP or DIAG out of the row; column 0 is TOP (:78-79). The
+// staged masks nl / dg hold per strip row one bit per slot (R = 1 slot e = x - 1 + k of column x at bit
+// e % 32 of word 1 + e / 32 - clo; word 0 is zero; not LEFT / DIAG); the nearest set nl bit at or
+// below the entry's is the cell the row leaves from. The LEFT runs tb_step's probe does not cover: the
+// entry's word, then the nearest nonzero word below it from the row's nonzero-word mask nz; -1
+// (unknown: the table entry invalid, so a path through it falls back to the sequential walk) when the
+// entry or the run leaves the staged chunks.
+__device__ __noinline__ int tb_row_slow(int x, int k, tb_lds_u32 *nl, tb_lds_u32 *dg, tb_lds_u32 *nz, int clo, int nch)
+{
+    const int e = x - 1 + k;
+    int i = (e >> 5) - clo;
+    if ((unsigned)i >= (unsigned)nch) return -1;
+    uint32_t w = nl[k * kTbRow + 1 + i] & (0xffffffffu >> (31 - (e & 31)));
+    if (!w)
+    {
+        // the highest staged word below i with a set bit
+        int j = -1;
+        for (int q = (i - 1) >> 5; q >= 0 && j < 0 && i > 0; --q)
+        {
+            uint32_t z = nz[k * kTbNz + q];
+            if (q == (i - 1) >> 5) z &= 0xffffffffu >> (31 - ((i - 1) & 31));
+            if (z) j = 32 * q + 31 - __builtin_clz(z);
+        }
+        if (j < 0) return clo * 32 <= k ? 0 : -1;  // none: column 0 if the staged slots reach it
+        i = j;
+        w = nl[k * kTbRow + 1 + i];
+    }
+    const int pos = 31 - __builtin_clz(w);
+    const int col = (i + clo) * 32 + pos + 1 - k;
+    return col <= 0 ? 0 : col - (int)((dg[k * kTbRow + 1 + i] >> pos) & 1u);
+}
+
+// One row for a chain at column x (0: column 0, which stays there; -1: unknown, stays unknown). The
+// entry's word and the one below it (64 slots as one 64-bit word) cover the 33 .. 64 slots at and left
+// of the entry; a longer LEFT run, or an entry outside the staged chunks, goes through tb_row_slow.
+__device__ __forceinline__ int tb_step(int x, int k, tb_lds_u32 *nl, tb_lds_u32 *dg, tb_lds_u32 *nz, int clo, int nch)
 {
     const int e = x - 1 + k, i = (e >> 5) - clo, bit = e & 31;
-    const bool in = x > 0 && (unsigned)i < (unsigned)nch && (i >= 1 || clo == 0);
-    const int ih = in ? k * kTbRow + i : 0, il = in && i >= 1 ? ih - 1 : ih;
-    const uint32_t nh = nl[ih] & (0xffffffffu >> (31 - bit)), dh = dg[ih];
-    const uint32_t nlo = i >= 1 ? nl[il] : 0u, dlo = dg[il];
-    const int ph = nh ? 31 - __builtin_clz(nh) : 0, pl = nlo ? 31 - __builtin_clz(nlo) : 0;
-    const int slot = nh ? e - bit + ph : (nlo ? e - bit - 32 + pl : INT_MIN);
-    const int d = nh ? (int)((dh >> ph) & 1u) : (int)((dlo >> pl) & 1u);
-    const int col = slot + 1 - k;
-    // nothing found: column 0 when the two words reach it (slot k - 1), else the slow walk
-    const int low = e - bit - (i >= 1 ? 32 : 0);
-    int r = slot != INT_MIN ? (col <= 0 ? 0 : col - d) : (low <= k ? 0 : -1);
-    if (!in) r = x > 0 ? -1 : 0;
-    return r >= 0 ? r : tb_row_slow(x, k, gb);
+    const bool in = x > 0 && (unsigned)i < (unsigned)nch;
+    const int a = k * kTbRow + 1 + (in ? i : 0);
+    const uint64_t W = ((uint64_t)(nl[a] & (0xffffffffu >> (31 - bit))) << 32) | nl[a - 1];
+    const uint64_t G = ((uint64_t)dg[a] << 32) | dg[a - 1];
+    const int pos = 63 - __builtin_clzll(W | 1);
+    const int col = e - bit - 32 + pos + 1 - k;
+    const int d = (int)((G >> pos) & 1u);
+    // nothing found: column 0 when the two words reach it (word 0 is real only when clo is 0)
+    const bool reach = (i >= 1 || clo == 0) && e - bit - 32 <= k;
+    int r = W ? (col <= 0 ? 0 : col - d) : (reach ? 0 : -2);
+    if (!in) r = x > 0 ? -2 : x;
+    return r != -2 ? r : tb_row_slow(x, k, nl, dg, nz, clo, nch);
 }
 
 // Compaction of the distinct chains (tb_table_kernel): chains that met stay equal, and each run of
 // equal values in cur[0 .. D) becomes one chain (values of different runs may repeat: they stay apart,
-// which costs work, not correctness); map[] (start column -> chain) follows. Returns the new D.
+// which costs work, not correctness); map[] (start column -> chain) follows. Thread t holds elements
+// E t .. E t + E - 1. Returns the new D.
+template <int E>
 __device__ __forceinline__ int tb_compact(int *cur, uint16_t *map, uint16_t *tmp, int *wsum, int D)
 {
-    const int t = threadIdx.x, i0 = 2 * t, i1 = 2 * t + 1;
-    const int v0 = i0 < D ? cur[i0] : 0, v1 = i1 < D ? cur[i1] : 0;
-    const int vp = i0 > 0 && i0 < D ? cur[i0 - 1] : 0;
-    const int f0 = i0 < D && (i0 == 0 || v0 != vp), f1 = i1 < D && v1 != v0;
-    const int f = f0 + f1;
+    const int t = threadIdx.x, i0 = E * t;
+    int v[E], fl[E];
+    int prev = i0 > 0 && i0 < D ? cur[i0 - 1] : 0, f = 0;
+    for (int q = 0; q < E; ++q)
+    {
+        v[q] = i0 + q < D ? cur[i0 + q] : 0;
+        fl[q] = i0 + q < D && (i0 + q == 0 || v[q] != prev);
+        prev = v[q];
+        f += fl[q];
+    }
     const int inc = wave_prefix_sum(f);
     const int wv = t / kWave;
     if ((t & (kWave - 1)) == kWave - 1) wsum[wv] = inc;
@@ -1162,13 +1176,18 @@ __device__ __forceinline__ int tb_compact(int *cur, uint16_t *map, uint16_t *tmp
         before += k < wv ? x : 0;
         total += x;
     }
-    const int n0 = before + inc - f + f0 - 1, n1 = n0 + f1;  // new chain of elements i0, i1
-    if (i0 < D) tmp[i0] = (uint16_t)n0;
-    if (i1 < D) tmp[i1] = (uint16_t)n1;
+    int nidx[E];
+    int c = before + inc - f - 1;  // new chain of the element before i0
+    for (int q = 0; q < E; ++q)
+    {
+        c += fl[q];
+        nidx[q] = c;
+        if (i0 + q < D) tmp[i0 + q] = (uint16_t)c;
+    }
     __syncthreads();  // (every read of cur and wsum is done)
-    if (f0) cur[n0] = v0;
-    if (f1) cur[n1] = v1;
-    for (int c = t; c < kTbK; c += blockDim.x) map[c] = tmp[map[c]];
+    for (int q = 0; q < E; ++q)
+        if (fl[q]) cur[nidx[q]] = v[q];
+    for (int e = t; e < kTbK; e += blockDim.x) map[e] = tmp[map[e]];
     __syncthreads();
     return total;
 }
@@ -1178,9 +1197,10 @@ __device__ __forceinline__ int tb_compact(int *cur, uint16_t *map, uint16_t *tmp
 // strip's last down to its first. Chains that meet stay merged, so after 4 and after 16 rows the
 // distinct ones are compacted (2048 -> ~500 -> ~230 at 32768^2 random DNA) and only those walk on.
 constexpr int kTbPhases = 3;
-__global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
+constexpr int kTbThreads = 512;
+__global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
 {
-    __shared__ uint32_t nlm[kWave * kTbRow], dgm[kWave * kTbRow];
+    __shared__ uint32_t nlm[kWave * kTbRow], dgm[kWave * kTbRow], nzm[kWave * kTbNz];
     __shared__ int cur[kTbK];
     __shared__ uint16_t map[kTbK], tmp[kTbK];
     __shared__ int wsum[16];
@@ -1196,15 +1216,35 @@ __global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
     const int kTop = b == bs ? (i0 - 1) & 63 : 63;
     const int lo = tb_window_lo(b, n, m, i0, j0, a.local != 0);
     if (threadIdx.x == 0) a.win[s] = lo;
+    if (a.dbg && threadIdx.x == 0) a.dbg[12 * (size_t)s] = __builtin_amdgcn_s_memrealtime();
     const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
     const int clo = max(0, (lo - 1 - kTbMargin) >> 5);
     const int nch = max(0, min(kTbChunks, (uniform(sd.nsteps) >> 5) - clo));
-    for (int e = threadIdx.x; e < nch * kWave; e += blockDim.x)
+    if (threadIdx.x < kWave)
     {
-        const int q = e / kWave, k = e % kWave;  // chunk, strip lane: its two raw words (slots 0-15, 16-31)
-        const u32x2 v = *reinterpret_cast<const u32x2 *>(sb + ((int64_t)clo + q) * kChunkDw + 2 * k);
-        nlm[k * kTbRow + q] = tb_slots16(v.x | (v.x >> 1)) | (tb_slots16(v.y | (v.y >> 1)) << 16);
-        dgm[k * kTbRow + q] = tb_slots16(v.x >> 1) | (tb_slots16(v.y >> 1) << 16);
+        nlm[threadIdx.x * kTbRow] = dgm[threadIdx.x * kTbRow] = 0;
+        for (int q = 0; q < kTbNz; ++q) nzm[threadIdx.x * kTbNz + q] = 0;
+    }
+    __syncthreads();
+    constexpr int kStageBatch = 4;  // raw loads in flight per thread
+    for (int e0 = threadIdx.x; e0 < nch * kWave; e0 += kStageBatch * blockDim.x)
+    {
+        u32x2 v[kStageBatch];
+        for (int u = 0; u < kStageBatch; ++u)
+        {
+            const int e = e0 + u * blockDim.x;  // chunk e / 64, strip lane e % 64: its two raw words
+            v[u] = e < nch * kWave ? *reinterpret_cast<const u32x2 *>(sb + ((int64_t)clo + e / kWave) * kChunkDw + 2 * (e % kWave))
+                                   : u32x2{0u, 0u};
+        }
+        for (int u = 0; u < kStageBatch; ++u)
+        {
+            const int e = e0 + u * blockDim.x, q = e / kWave, k = e % kWave;
+            if (e >= nch * kWave) break;
+            const uint32_t nlw = tb_slots16(v[u].x | (v[u].x >> 1)) | (tb_slots16(v[u].y | (v[u].y >> 1)) << 16);
+            nlm[k * kTbRow + 1 + q] = nlw;
+            dgm[k * kTbRow + 1 + q] = tb_slots16(v[u].x >> 1) | (tb_slots16(v[u].y >> 1) << 16);
+            if (nlw) atomicOr(&nzm[k * kTbNz + (q >> 5)], 1u << (q & 31));
+        }
     }
     for (int t = threadIdx.x; t < kTbK; t += blockDim.x)
     {
@@ -1214,7 +1254,10 @@ __global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
     __syncthreads();
     tb_lds_u32 *nl = (tb_lds_u32 *)nlm;
     tb_lds_u32 *dg = (tb_lds_u32 *)dgm;
-    tb_glb_u32 *gb = (tb_glb_u32 *)sb;
+    tb_lds_u32 *nz = (tb_lds_u32 *)nzm;
+    uint64_t stamp[12] = {};
+    const bool dbg = a.dbg != nullptr;
+    if (dbg) stamp[0] = __builtin_amdgcn_s_memrealtime();
     constexpr int kRowsBefore[kTbPhases] = {4, 16, 64};  // rows walked before each compaction
     int D = kTbK, k = kTop;
     for (int ph = 0; ph < kTbPhases; ++ph)
@@ -1223,16 +1266,28 @@ __global__ __launch_bounds__(1024) void tb_table_kernel(TbArgs a)
         for (int t = threadIdx.x; t < D; t += blockDim.x)
         {
             int x = cur[t];
-            for (int kk = k; kk > kEnd; --kk) x = tb_step(x, kk, nl, dg, clo, nch, gb);
+            for (int kk = k; kk > kEnd; --kk) x = tb_step(x, kk, nl, dg, nz, clo, nch);
             cur[t] = x;
         }
         k = kEnd;
         __syncthreads();
+        if (dbg) stamp[1 + 3 * ph] = __builtin_amdgcn_s_memrealtime();
         if (k < 0) break;
-        D = tb_compact(cur, map, tmp, wsum, D);
+        D = tb_compact<kTbK / kTbThreads>(cur, map, tmp, wsum, D);
+        if (dbg)
+        {
+            stamp[2 + 3 * ph] = __builtin_amdgcn_s_memrealtime();
+            stamp[3 + 3 * ph] = (uint64_t)D;
+        }
     }
     int32_t *out = a.tbl + (int64_t)s * kTbK;
     for (int t = threadIdx.x; t < kTbK; t += blockDim.x) out[t] = lo + t <= n ? cur[map[t]] : -1;
+    if (dbg && threadIdx.x == 0)
+    {
+        stamp[10] = __builtin_amdgcn_s_memrealtime();
+        stamp[11] = a.dbg[12 * (size_t)s];  // (the kernel entry stamp, written at the start)
+        for (int e = 0; e < 12; ++e) a.dbg[12 * (size_t)s + e] = stamp[e];
+    }
 }
 
 // Copies tables t0 .. t0 + nt - 1 (kTbK int32 each) of src into LDS (all threads of the block)
@@ -1779,7 +1834,7 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
 void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st)
 {
     hipLaunchKernelGGL(tb_start_kernel, dim3(np), dim3(kWave), 0, st, a);
-    hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(1024), 0, st, a);
+    hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(kTbThreads), 0, st, a);
     hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
     hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
