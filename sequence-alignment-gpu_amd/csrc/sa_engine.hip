@@ -204,6 +204,7 @@ struct Knobs {
     bool tb_generic = false;        // SA_TB_GENERIC: row walk without the unrolled strip code
     bool tb_stager = true;          // SA_TB_STAGER=0: the row walker stages every strip itself
     bool tb_tables = true;          // SA_TB_TABLES=0: no table traceback (every pair walks sequentially)
+    int tb_rounds = 0;              // SA_TB_ROUNDS: rounds of tables (default: plan_traceback)
     bool tb_strict = false;         // SA_TB_STRICT: no sequential walk after the table traceback
                                     // (tests: a pair it left keeps a stale head and fails its check)
     int max_cus = 0;                // SA_MAX_CUS: plan as if the device had at most this many CUs (tests)
@@ -232,6 +233,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_TB_STAGER")) v.tb_stager = std::atoi(e) != 0;
         if (const char *e = get("SA_TB_TABLES")) v.tb_tables = std::atoi(e) != 0;
         v.tb_strict = get("SA_TB_STRICT") != nullptr;
+        if (const char *e = get("SA_TB_ROUNDS")) v.tb_rounds = std::max(0, std::atoi(e));
         if (const char *e = get("SA_MAX_CUS")) v.max_cus = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
@@ -903,7 +905,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_gent, sizeof(int32_t) * ntg},
         {(void **)&pl->d_tbflag, ntg ? sizeof(int32_t) * npp : 0},
         {(void **)&pl->d_win, ntg ? sizeof(int32_t) * nstr : 0},
-        {(void **)&pl->d_tbstart, ntg ? sizeof(int32_t) * 4 * npp : 0},
+        {(void **)&pl->d_tbstart, ntg ? sizeof(int32_t) * kTbStartWords * npp : 0},
         {(void **)&pl->d_pend, ntg ? sizeof(int32_t) * npp : 0},
         {(void **)&pl->d_sent, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * nstr : 0},
         {(void **)&pl->d_sdelta, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * nstr : 0},
@@ -1205,7 +1207,11 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         t.rec = pl->d_rec;
         t.heads = pl->d_heads;
         t.fast = w.fast;
-        launch_tb(t, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, st);
+        // rounds of tables: pairs past 131072 rows stray further from the first round's line than its
+        // windows reach (random DNA: 800 columns at 120000^2, 3000 at 250000^2; tools/path_deviation.py);
+        // a round with nothing pending costs its three launches
+        const int rounds = kn.tb_rounds > 0 ? kn.tb_rounds : (pl->max_recs > 131072 ? 8 : 1);
+        launch_tb(t, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, rounds, st);
         HIP_TRY(hipGetLastError());
         if (kn.tb_table_timing)
         {

@@ -66,6 +66,22 @@ struct WalkArgs {
 constexpr int kTbK = 2048;       // start columns per strip window
 constexpr int kTbG = 16;         // strips per group
 constexpr int kTbMinStrips = 8;  // pairs with fewer strips take the sequential walk
+// ROUNDS. The windows of a round are centred on a line through an anchor: the start cell, then (a
+// round that found the path leaving a window at group g) the path's entry column into group g, which
+// is then known. The next round rebuilds the tables of the strips at and above the anchor and resumes
+// the chain at group g. Line: global, towards (0, 0) (where the path ends); local, the slope of the
+// path from the start cell to the anchor (slope 1 from the start cell in the first round: a local
+// alignment's own diagonal; towards (0, 0) measured worse for short ones). Local needs the path only
+// down to where traceBackSW ends: a local pair whose chain stops after some groups keeps the groups
+// resolved so far, and falls back only when the walk does not end inside them (tb_finish_kernel).
+// tb_flag: 0 resolved by the tables, 1 sequential walk, 2 pending (another round).
+enum TbStart {
+    kTbI0, kTbJ0, kTbH, kTbBs,       // start cell, its H, its strip
+    kTbRa, kTbXa, kTbDr, kTbDx,      // anchor row / column, line slope dx / dr (columns per row)
+    kTbGres,                         // group the chain resumes at (-1: the start cell's group)
+    kTbBmin,                         // local: the lowest strip resolved (the walk may end above it)
+    kTbStartWords = 12
+};
 struct TbGroup {
     int32_t pair, s_lo, s_hi, pad;  // the plan's strip indices, s_lo <= s_hi (one pair's)
 };
@@ -77,7 +93,7 @@ struct TbArgs {
     const int32_t *pair_g0;  // [np + 1]: pair p's groups are pair_g0[p] .. pair_g0[p + 1] - 1
     const int32_t *pair_score;
     const uint64_t *strip_best;  // local: best-cell key per strip
-    int32_t *start;          // [pair][4] start cell i, j, its H, its strip (tb_start_kernel)
+    int32_t *start;          // [pair][kTbStartWords] (tb_start_kernel, tb_resolve_kernel; TbStart)
     int32_t *tbl;            // [strip][kTbK] exit column (-1: start column past n)
     int32_t *win;            // [strip] first column of the strip's window (tb_table_kernel)
     int32_t *gtbl;           // [group][kTbK] exit column of the group (-1: left a window)
@@ -93,20 +109,20 @@ struct TbArgs {
     const int8_t *text, *pattern;
     const int32_t *score_tab;  // A x A, S + g (the plan's local table)
     int32_t A, gap, key_rowbits, local, fast;
+    int32_t last_round;        // the last round of tables (a pair still unresolved falls back)
     uint64_t *dbg;             // debug (SA_TB_TABLE_TIMING): per strip 12 words of tb_table_kernel stamps
 };
 
-// First column of strip b's window: kTbK columns centred, at the strip's first walked row r, on the
-// diagonal through (m, n) and (0, 0) (global) or on the slope-1 line through the start cell (i0, j0)
-// (local), clamped to the pair's columns
-__host__ __device__ inline int tb_window_lo(int b, int n, int m, int i0, int j0, bool local)
+// First column of strip b's window: kTbK columns centred, at the strip's first walked row
+// r = min(64 b + 64, i0), on the line x = xa - (ra - r) dx / dr (TbStart), clamped to the pair's columns
+__host__ __device__ inline int tb_window_lo(int b, int n, int i0, int ra, int xa, int dr, int dx)
 {
     const int64_t r = b * 64 + 64 < i0 ? b * 64 + 64 : i0;
-    const int64_t c = (local ? (int64_t)j0 - (i0 - r) : (r * n + m / 2) / m) - kTbK / 2;
+    const int64_t c = xa - (((int64_t)(ra - r) * dx + dr / 2) / dr) - kTbK / 2;
     const int64_t hi = n + 1 - kTbK > 0 ? n + 1 - kTbK : 0;
     return (int)(c < 0 ? 0 : (c > hi ? hi : c));
 }
-void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st);
+void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, int rounds, hipStream_t st);
 
 struct ExpandArgs {
     const int8_t *text, *pattern;

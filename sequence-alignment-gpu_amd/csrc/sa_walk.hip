@@ -1207,14 +1207,15 @@ __global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
     const int s = blockIdx.x;
     const StripDesc sd = a.strips[s];
     const int p = uniform(sd.pair);
-    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 0) return;  // (sequential walk)
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 2) return;  // (not pending)
     const PairDesc pd = a.pairs[p];
-    const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
-    const int i0 = uniform(a.start[4 * p]), j0 = uniform(a.start[4 * p + 1]), bs = uniform(a.start[4 * p + 3]);
+    const int n = uniform((int)pd.text_len);
+    const int32_t *st = a.start + kTbStartWords * p;
+    const int i0 = uniform(st[kTbI0]), bs = uniform(st[kTbBs]), ra = uniform(st[kTbRa]);
     const int b = s - uniform(pd.first_strip);
-    if (b > bs) return;  // (below the start cell)
+    if (b > (ra - 1) >> 6) return;  // (below the anchor: resolved, or below the start cell)
     const int kTop = b == bs ? (i0 - 1) & 63 : 63;
-    const int lo = tb_window_lo(b, n, m, i0, j0, a.local != 0);
+    const int lo = tb_window_lo(b, n, i0, ra, uniform(st[kTbXa]), uniform(st[kTbDr]), uniform(st[kTbDx]));
     if (threadIdx.x == 0) a.win[s] = lo;
     if (a.dbg && threadIdx.x == 0) a.dbg[12 * (size_t)s] = __builtin_amdgcn_s_memrealtime();
     const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
@@ -1299,8 +1300,9 @@ __device__ __forceinline__ void tb_stage_tables(int32_t *dst, const int32_t *src
 }
 
 // One wave per pair: the start cell (global: (m, n); local: the best cell, from the strips' keys as
-// walk_start), the strip holding it; tb_flag = 1 for the pairs of the sequential walk (no groups, or a
-// local pair without a positive cell: its empty alignment)
+// walk_start), the strip holding it, the first round's anchor; tb_flag = 2 (pending), or 1 for the
+// pairs of the sequential walk (no groups, or a local pair without a positive cell: its empty
+// alignment)
 __global__ __launch_bounds__(kWave) void tb_start_kernel(TbArgs a)
 {
     const int p = blockIdx.x, lane = threadIdx.x;
@@ -1324,12 +1326,19 @@ __global__ __launch_bounds__(kWave) void tb_start_kernel(TbArgs a)
     else if (ok)
         H = a.pair_score[p];
     if (lane != 0) return;
-    a.tb_flag[p] = ok ? 0 : 1;
+    a.tb_flag[p] = ok ? 2 : 1;
     if (!ok) return;
-    a.start[4 * p] = i;
-    a.start[4 * p + 1] = j;
-    a.start[4 * p + 2] = H;
-    a.start[4 * p + 3] = (i - 1) >> 6;
+    int32_t *st = a.start + kTbStartWords * p;
+    st[kTbI0] = i;
+    st[kTbJ0] = j;
+    st[kTbH] = H;
+    st[kTbBs] = (i - 1) >> 6;
+    st[kTbRa] = i;  // the first round's line: through (m, n) and (0, 0) / slope 1 from the best cell
+    st[kTbXa] = j;
+    st[kTbDr] = a.local ? 1 : i;
+    st[kTbDx] = a.local ? 1 : j;
+    st[kTbGres] = -1;
+    st[kTbBmin] = 0;
     a.pend[p] = -1;
 }
 
@@ -1337,7 +1346,7 @@ __global__ __launch_bounds__(kWave) void tb_start_kernel(TbArgs a)
 __device__ __forceinline__ bool tb_group_span(const TbArgs &a, const TbGroup &g, const PairDesc &pd, int &sLo, int &sHi)
 {
     sLo = uniform(g.s_lo);
-    sHi = min(uniform(g.s_hi), uniform(pd.first_strip) + uniform(a.start[4 * uniform(g.pair) + 3]));
+    sHi = min(uniform(g.s_hi), uniform(pd.first_strip) + uniform(a.start[kTbStartWords * uniform(g.pair) + kTbBs]));
     return sHi >= sLo;
 }
 
@@ -1348,7 +1357,9 @@ __global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
     __shared__ int32_t tl[kTbG * kTbK];
     __shared__ int wl[kTbG];
     const TbGroup g = a.groups[blockIdx.x];
-    if (uniform(a.tb_flag[uniform(g.pair)]) != 0) return;
+    if (uniform(a.tb_flag[uniform(g.pair)]) != 2) return;
+    const int gres = uniform(a.start[kTbStartWords * uniform(g.pair) + kTbGres]);
+    if (gres >= 0 && (int)blockIdx.x > gres) return;  // (resolved in an earlier round)
     const PairDesc pd = a.pairs[uniform(g.pair)];
     int sLo, sHi;
     if (!tb_group_span(a, g, pd, sLo, sHi)) return;
@@ -1369,61 +1380,95 @@ __global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
     }
 }
 
-// One block per pair: the group tables chained from the start cell upward (staged in LDS kTbG at a
-// time) give every group's entry column and the row-0 column; global: the pair's head (the trailing
-// LEFT run). A column outside a window: tb_flag = 1 and walk_rw_kernel walks the pair instead.
+// One block per pair (pending): the group tables chained from the anchor's group upward (staged in LDS
+// kTbG at a time) give every group's entry column and the row-0 column; global: the pair's head (the
+// trailing LEFT run). A column outside a window at group g: the next round anchors at g's entry
+// (TbStart), unless this is the last round or g was the round's first group (no progress): then
+// tb_flag = 1 and walk_rw_kernel walks the pair instead.
 __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
 {
     __shared__ int32_t tl[kTbG * kTbK];
-    __shared__ int xs;
+    __shared__ int xs, gfail, xfail;
     const int p = blockIdx.x;
-    if (uniform(a.tb_flag[p]) != 0) return;
-    const int g0 = uniform(a.pair_g0[p]), g1 = uniform(a.pair_g0[p + 1]);
+    if (uniform(a.tb_flag[p]) != 2) return;
+    const int g0 = uniform(a.pair_g0[p]);
     const PairDesc pd = a.pairs[p];
-    const int first = uniform(pd.first_strip), bs = uniform(a.start[4 * p + 3]);
-    // the groups walked: g0 .. gs (gs holds the start cell's strip)
-    int gs = g1 - 1;
-    while (gs > g0 && uniform(a.groups[gs].s_lo) > first + bs) --gs;
-    if (threadIdx.x == 0) xs = a.start[4 * p + 1];
+    const int first = uniform(pd.first_strip);
+    int32_t *st = a.start + kTbStartWords * p;
+    const int i0 = uniform(st[kTbI0]), bs = uniform(st[kTbBs]);
+    // the start cell's group, and the round's first group: the anchor's, or the start cell's
+    int gstart = uniform(a.pair_g0[p + 1]) - 1;
+    while (gstart > g0 && uniform(a.groups[gstart].s_lo) > first + bs) --gstart;
+    const int gs = uniform(st[kTbGres]) >= 0 ? uniform(st[kTbGres]) : gstart;
+    if (threadIdx.x == 0)
+    {
+        xs = st[kTbXa];
+        gfail = -1;
+    }
     for (int gh = gs + 1; gh > g0; gh -= kTbG)
     {
         const int gl = max(g0, gh - kTbG);
         __syncthreads();  // (the previous chunk's lookups are done)
+        if (uniform(gfail) >= 0) break;
         tb_stage_tables(tl, a.gtbl, gl, gh - gl);
         __syncthreads();
         if (threadIdx.x == 0)
         {
             int x = xs;
-            for (int g = gh - 1; g >= gl && x >= 0; --g)
+            for (int g = gh - 1; g >= gl; --g)
             {
                 const int lo = a.win[min(a.groups[g].s_hi, first + bs)];
-                if (x < lo || x >= lo + kTbK)
-                    x = -1;
-                else
+                const int y = (x >= lo && x < lo + kTbK) ? tl[(g - gl) * kTbK + x - lo] : -1;
+                if (y < 0)
                 {
-                    a.gent[g] = x;
-                    x = tl[(g - gl) * kTbK + x - lo];
+                    gfail = g;  // the path's entry into group g is x; it leaves a window at or in g
+                    xfail = x;
+                    break;
                 }
+                a.gent[g] = x;
+                x = y;
             }
             xs = x;
         }
     }
     __syncthreads();
     if (threadIdx.x != 0) return;
-    const int x = xs;
-    if (x < 0)
+    if (gfail >= 0)
     {
-        a.tb_flag[p] = 1;
+        if (a.last_round || gfail == gs)
+        {
+            // local: groups gfail + 1 .. gstart are resolved, and the walk may end in them
+            const bool keep = a.local && gfail < gstart;
+            a.tb_flag[p] = keep ? 0 : 1;
+            if (keep) st[kTbBmin] = a.groups[gfail + 1].s_lo - first;
+            return;
+        }
+        // the next round: anchor at group gfail's entry (its first walked row)
+        const int r = min(64 * (min(a.groups[gfail].s_hi, first + bs) - first) + 64, i0);
+        st[kTbRa] = r;
+        st[kTbXa] = xfail;
+        if (a.local)
+        {
+            st[kTbDr] = i0 - r;  // (> 0: the chain progressed past the start cell's group)
+            st[kTbDx] = st[kTbJ0] - xfail;
+        }
+        else
+        {
+            st[kTbDr] = r;
+            st[kTbDx] = xfail;
+        }
+        st[kTbGres] = gfail;
         return;
     }
+    a.tb_flag[p] = 0;
     if (a.local) return;  // (the head: tb_finish_kernel)
     TbHead h;
     h.kind = kRecRows;
     h.tail_op = kLeft;
-    h.tail = x;  // row 0: LEFT to column 0 (traceBackNW :80-81)
+    h.tail = xs;  // row 0: LEFT to column 0 (traceBackNW :80-81)
     h.nrec = (int)pd.pattern_len;
     h.pad = 0;
-    h.score = a.start[4 * p + 2];
+    h.score = st[kTbH];
     h.i0 = (int)pd.pattern_len;
     h.j0 = (int)pd.text_len;
     h.start_text = 0;
@@ -1446,7 +1491,8 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
     int sLo, sHi;
     if (!tb_group_span(a, g, pd, sLo, sHi)) return;
     const int first = uniform(pd.first_strip);
-    const int i0 = uniform(a.start[4 * p]), bs = uniform(a.start[4 * p + 3]);
+    const int i0 = uniform(a.start[kTbStartWords * p + kTbI0]), bs = uniform(a.start[kTbStartWords * p + kTbBs]);
+    if (sLo < first + uniform(a.start[kTbStartWords * p + kTbBmin])) return;  // (local: not resolved)
     tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
     __syncthreads();
     if (threadIdx.x == 0)
@@ -1510,12 +1556,12 @@ __global__ __launch_bounds__(kWave) void tb_check_kernel(TbArgs a)
     if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 0) return;
     const PairDesc pd = a.pairs[p];
     const int first = uniform(pd.first_strip);
-    const int i0 = uniform(a.start[4 * p]), bs = uniform(a.start[4 * p + 3]);
+    const int i0 = uniform(a.start[kTbStartWords * p + kTbI0]), bs = uniform(a.start[kTbStartWords * p + kTbBs]);
     const int b = s - first;
-    if (b > bs) return;
+    if (b > bs || b < uniform(a.start[kTbStartWords * p + kTbBmin])) return;  // (not walked / not resolved)
     int hsum = 0;
     for (int q = b + 1 + lane; q <= bs; q += kWave) hsum += a.sdelta[first + q];
-    const int Hc = uniform(a.start[4 * p + 2]) + __builtin_amdgcn_readlane(wave_prefix_sum(hsum), kWave - 1);
+    const int Hc = uniform(a.start[kTbStartWords * p + kTbH]) + __builtin_amdgcn_readlane(wave_prefix_sum(hsum), kWave - 1);
     const int kTop = b == bs ? (i0 - 1) & 63 : 63;
     const int jc = uniform(a.sent[s]);
     const int cn0 = i0 - (64 * b + kTop + 1);
@@ -1561,9 +1607,9 @@ __global__ __launch_bounds__(kWave) void tb_finish_kernel(TbArgs a)
     h.start_text = a.send[4 * s + 2];
     h.start_pattern = a.send[4 * s + 3];
     h.pad = 0;
-    h.score = a.start[4 * p + 2];
-    h.i0 = a.start[4 * p];
-    h.j0 = a.start[4 * p + 1];
+    h.score = a.start[kTbStartWords * p + kTbH];
+    h.i0 = a.start[kTbStartWords * p + kTbI0];
+    h.j0 = a.start[kTbStartWords * p + kTbJ0];
     a.heads[p] = h;
 }
 
@@ -1831,12 +1877,17 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
     else launch_walk_m<false>(R, a, np, st);
 }
 
-void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, hipStream_t st)
+void launch_tb(const TbArgs &args, int nstrips, int ngroups, int np, int rounds, hipStream_t st)
 {
+    TbArgs a = args;
     hipLaunchKernelGGL(tb_start_kernel, dim3(np), dim3(kWave), 0, st, a);
-    hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(kTbThreads), 0, st, a);
-    hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
-    hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
+    for (int r = 1; r <= rounds; ++r)
+    {
+        a.last_round = r == rounds;
+        hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(kTbThreads), 0, st, a);
+        hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
+        hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
+    }
     hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
     if (a.local)
     {
