@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--rows-per-lane", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
+    ap.add_argument("--batch-pipeline", type=int, default=1,
+                    help="batch, one rank: overlap step k's traceback with step k+1's fill (two plan copies)")
     ap.add_argument("--batch-chunks", type=int, default=1,
                     help="batch: plans per rank; chunk k's traceback overlaps chunk k+1's fill")
     ap.add_argument("--dry-run", action="store_true",
@@ -200,6 +202,53 @@ class Chunked:
             bad = int(np.flatnonzero(res["status"])[0])
             raise RuntimeError(f"pair {bad} has status {int(res['status'][bad])}")
         return res
+
+
+class Pipelined:
+    """--workload batch, one rank: two copies of the rank's plans (the same pairs, each with its own
+    direction planes) so that batch steps overlap two deep. Step k fills copy k % 2 on the fill stream
+    once that copy's previous traceback (step k - 2) has read its planes; step k - 1's results come to
+    the host while step k's fill runs; then step k's traceback goes on the traceback stream behind its
+    fill. Every step still fills, traces back and returns all of its pairs (the VALU-bound fill and
+    the gather-bound traceback share the CUs)."""
+
+    def __init__(self, a: Chunked, b: Chunked, torch, local):
+        self.sets, self.torch = [a, b], torch
+        self.s_fill = torch.cuda.current_stream(local)
+        self.s_tb = torch.cuda.Stream(local)
+        self.fill_done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.tb_done = [torch.cuda.Event(), torch.cuda.Event()]
+        self.k, self.pending = 0, None
+
+    def step(self, ev=None) -> None:
+        i = self.k % 2
+        jobs = self.sets[i].jobs
+        if self.k >= 2:
+            self.s_fill.wait_event(self.tb_done[i])
+        if ev is not None:
+            ev[0].record(self.s_fill)
+        for j in jobs:
+            j.plan.fill(j.d_text.data_ptr(), j.d_pattern.data_ptr(), self.s_fill.cuda_stream)
+        if ev is not None:
+            ev[1].record(self.s_fill)
+        self.fill_done[i].record(self.s_fill)
+        self.drain()
+        self.s_tb.wait_event(self.fill_done[i])
+        for j in jobs:
+            j.plan.traceback(self.s_tb.cuda_stream)
+        self.tb_done[i].record(self.s_tb)
+        self.pending = i
+        self.k += 1
+
+    def drain(self) -> None:
+        """The pending step's results to the host (waits for its traceback only)."""
+        if self.pending is None:
+            return
+        res = np.concatenate([j.plan.results_array(self.s_tb.cuda_stream) for j in self.sets[self.pending].jobs])
+        if len(res) and res["status"].any():
+            bad = int(np.flatnonzero(res["status"])[0])
+            raise RuntimeError(f"pair {bad} has status {int(res['status'][bad])}")
+        self.pending = None
 
 
 def main_native(args) -> None:
@@ -353,13 +402,19 @@ def main():
         chunks = [DeviceBatch(0, S, gap, texts[a:b], pats[a:b], device=local, rows_per_lane=args.rows_per_lane)
                   for a, b in zip(cuts, cuts[1:]) if b > a]
         job = Chunked(chunks, torch, local)
+        pipe = None
+        if args.batch_pipeline and world == 1 and len(chunks) == 1:
+            twin = Chunked([DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)], torch, local)
+            pipe = Pipelined(job, twin, torch, local)
         # the rank's sa_result rows go device to device into this buffer and on to rank 0 (RCCL gather)
         gbuf = torch.full(((npairs + world - 1) // world, 4), -1, dtype=torch.int64, device=torch.device("cuda", local))
         cells_rank = len(mine) * L * L
         pairs_rank = len(mine)
         workload = {"workload": f"dna_global_batch_{npairs}x{L}x{L}", "pairs_total": npairs, "text_len": L,
                     "pattern_len": L, "score": "blast +5/-4", "gap": gap, "parallelism": f"pairs_sharded{world}",
-                    "chunks_per_gpu": len(chunks)}
+                    "chunks_per_gpu": len(chunks),
+                    "step_overlap": ("two-deep: step k's traceback and results overlap step k+1's fill "
+                                     "(two plan copies)") if pipe is not None else "none"}
     if not isinstance(job, Chunked):
         job = Chunked([job], torch, local)
     info = job.info()
@@ -371,7 +426,9 @@ def main():
         # the fill launches (the dominant kernel) are bracketed by HIP events on the stream the engine
         # launches them on (torch's current stream); the rest of a batch step is timed only by the
         # wall clock
-        if args.workload == "batch":
+        if args.workload == "batch" and pipe is not None:
+            pipe.step(ev)
+        elif args.workload == "batch":
             # whole batch job per step: fill + traceback of this rank's pairs (chunk k's traceback on
             # a second stream, overlapping chunk k+1's fill), results to host, and the path's exchange
             # step — every rank's results gathered to rank 0 over RCCL (xGMI)
@@ -386,8 +443,12 @@ def main():
         else:
             job.fill(ev)
 
+    if args.workload != "batch":
+        pipe = None
     for _ in range(args.warmup):
         step()
+    if pipe is not None:
+        pipe.drain()
     torch.cuda.synchronize(local)
     # a batch step builds 4096 result dicts on the host; the cyclic collector's periodic full passes
     # over the interpreter's objects (measured: one 38 ms pause every ~8 steps) are host noise, not
@@ -401,6 +462,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
+    if pipe is not None:
+        pipe.drain()  # (the last step's traceback and results, inside the timed region)
     torch.cuda.synchronize(local)
     if world > 1:
         dist.barrier()
