@@ -1166,10 +1166,11 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     w.pattern = pl->d_pattern_in;
     w.score_tab = pl->d_table;
     w.A = pl->A;
-    w.tb_flag = nullptr;
+    w.tb_pg = nullptr;
     if (!pl->tb_groups.empty())
     {
-        // table traceback first; the sequential walk then takes only the pairs it left (tb_flag)
+        // table traceback; its last kernel walks the pairs the tables leave, so the sequential walk
+        // runs only when some pair has no groups
         TbArgs t;
         t.strips = pl->d_strips;
         t.pairs = pl->d_pairs;
@@ -1211,7 +1212,10 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         // windows reach (random DNA: 800 columns at 120000^2, 3000 at 250000^2; tools/path_deviation.py);
         // a round with nothing pending costs its three launches
         const int rounds = kn.tb_rounds > 0 ? kn.tb_rounds : (pl->max_recs > 131072 ? 8 : 1);
-        launch_tb(t, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, rounds, st);
+        t.strict = kn.tb_strict ? 1 : 0;
+        t.round = 1;
+        w.tb_pg = pl->d_tbpg;
+        launch_tb(t, w, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, rounds, st);
         HIP_TRY(hipGetLastError());
         if (kn.tb_table_timing)
         {
@@ -1225,9 +1229,10 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
             }
         }
         if (int rc = debug_sync(st, "table traceback")) return rc;
-        w.tb_flag = pl->d_tbflag;
     }
-    if (!w.tb_flag || !kn.tb_strict) launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
+    bool sequential = pl->tb_groups.empty();
+    for (int64_t p = 0; p < np && !sequential; ++p) sequential = pl->tb_pg[p + 1] == pl->tb_pg[p];
+    if (sequential) launch_walk(pl->R, pl->mode == SA_LOCAL, w, np, st);
     HIP_TRY(hipGetLastError());
     if (int rc = debug_sync(st, "walk kernel")) return rc;
     ExpandArgs x;

@@ -47,8 +47,9 @@ struct WalkArgs {
     const int8_t *text, *pattern;  // the fill's inputs (alphabet indices)
     const int32_t *score_tab;      // A x A, S + g (the plan's local table)
     int32_t A;
-    // table traceback (R = 1, see TbGroup): walk_rw_kernel walks only the pairs whose tb_flag is set
-    const int32_t *tb_flag;        // null: every pair
+    // table traceback (R = 1, see TbGroup): walk_rw_kernel walks only the pairs without groups
+    // (tb_finish_kernel walks those the tables leave)
+    const int32_t *tb_pg;          // TbArgs::pair_g0, or null: every pair
 };
 
 // TABLE TRACEBACK (R = 1 plans; sa_walk.hip tb_*_kernel). The sequential walk of a long pair costs
@@ -109,7 +110,8 @@ struct TbArgs {
     const int8_t *text, *pattern;
     const int32_t *score_tab;  // A x A, S + g (the plan's local table)
     int32_t A, gap, key_rowbits, local, fast;
-    int32_t last_round;        // the last round of tables (a pair still unresolved falls back)
+    int32_t round, last_round;  // this launch's round of tables (1 ..); the last (a pair still unresolved falls back)
+    int32_t strict;             // tests (SA_TB_STRICT): no sequential walk for the pairs the tables leave
     uint64_t *dbg;             // debug (SA_TB_TABLE_TIMING): per strip 12 words of tb_table_kernel stamps
 };
 
@@ -122,7 +124,9 @@ __host__ __device__ inline int tb_window_lo(int b, int n, int i0, int ra, int xa
     const int64_t hi = n + 1 - kTbK > 0 ? n + 1 - kTbK : 0;
     return (int)(c < 0 ? 0 : (c > hi ? hi : c));
 }
-void launch_tb(const TbArgs &a, int nstrips, int ngroups, int np, int rounds, hipStream_t st);
+// the table traceback of a plan's pairs with groups; the pairs it leaves are walked by tb_finish_kernel
+// with the row walk (w), so walk_rw_kernel need only run for pairs without groups
+void launch_tb(const TbArgs &a, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, hipStream_t st);
 
 struct ExpandArgs {
     const int8_t *text, *pattern;

@@ -637,19 +637,31 @@ __device__ void rw_stager_local(const WalkArgs &a, const PairDesc &sp, const uin
     }
 }
 
+// LDS of the row walk (walk_rw_pair)
 template <bool LOCAL>
-__global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
-{
-    __shared__ uint32_t pfbuf[2][kPfDw];
-    __shared__ uint32_t swin[2][kStageWin * kWave];
-    __shared__ int req[4];
-    __shared__ int stab[LOCAL ? 32 * 32 : 1];  // local: the substitution scores S (local_check)
+struct RwLds {
+    uint32_t pfbuf[2][kPfDw];
+    uint32_t swin[2][kStageWin * kWave];
+    int req[4];
+    int stab[LOCAL ? 32 * 32 : 1];  // local: the substitution scores S (local_check)
     // local: strips posted for local_check ([2][64 records + b, k, entry column, nrec before, H0]) and
     // the check's control words ([0] posted, [1] taken, [2] done, [3] ended, [4..7] nrec, tail, starts)
-    __shared__ int chkBuf[LOCAL ? 2 : 1][72];
-    __shared__ int chkCtl[8];
-    const int p = blockIdx.x;
-    if (a.tb_flag && uniform(a.tb_flag[p]) == 0) return;  // (the table traceback walked the pair)
+    int chkBuf[LOCAL ? 2 : 1][72];
+    int chkCtl[8];
+};
+
+// The row walk of pair p by a block of two waves (wave 0 the walker, wave 1 the stager); every thread
+// of the block calls it (it has a barrier). walk_rw_kernel, and tb_finish_kernel for the pairs the
+// table traceback leaves.
+template <bool LOCAL>
+__device__ __forceinline__ void walk_rw_pair(const WalkArgs &a, const int p, RwLds<LOCAL> &S)
+{
+    uint32_t(&pfbuf)[2][kPfDw] = S.pfbuf;
+    uint32_t(&swin)[2][kStageWin * kWave] = S.swin;
+    int *req = S.req;
+    int *stab = S.stab;
+    int(&chkBuf)[LOCAL ? 2 : 1][72] = S.chkBuf;
+    int *chkCtl = S.chkCtl;
     const int lane = threadIdx.x & (kWave - 1);
     if (threadIdx.x < 4) req[threadIdx.x] = 0;
     if (threadIdx.x < 8) chkCtl[threadIdx.x] = 0;
@@ -930,6 +942,15 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
     }
 }
 
+template <bool LOCAL>
+__global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
+{
+    __shared__ RwLds<LOCAL> S;
+    const int p = blockIdx.x;
+    if (a.tb_pg && uniform(a.tb_pg[p + 1]) > uniform(a.tb_pg[p])) return;  // (the table traceback's pairs)
+    walk_rw_pair<LOCAL>(a, p, S);
+}
+
 // Column walk (R >= 2): one wave per pair
 template <int R, bool LOCAL>
 __global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
@@ -1192,6 +1213,30 @@ __device__ __forceinline__ int tb_compact(int *cur, uint16_t *map, uint16_t *tmp
     return total;
 }
 
+// The start cell of pair p (global: (m, n); local: the best cell, from the strips' keys as walk_start)
+// and its H, by one wave; false for a local pair without a positive cell (its empty alignment: the
+// sequential walk)
+__device__ __forceinline__ bool tb_pair_start(const TbArgs &a, int p, const PairDesc &pd, int lane, int &i, int &j, int &H)
+{
+    i = (int)pd.pattern_len;
+    j = (int)pd.text_len;
+    if (!a.local)
+    {
+        H = a.pair_score[p];
+        return true;
+    }
+    const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
+    uint64_t k = 0;
+    for (int s = lane; s < nstrips; s += kWave) k = max(k, a.strip_best[first + s]);
+    k = wave_max_u64(k);
+    const int rb = a.key_rowbits;
+    const uint64_t km = (1ull << rb) - 1;
+    H = (int)(k >> (2 * rb));
+    i = (int)(km - ((k >> rb) & km));
+    j = (int)(km - (k & km));
+    return H > 0;
+}
+
 // Strip tables: block = one strip, 1024 threads, the kTbK start columns of the strip's window; the
 // strip's planes around the window staged in LDS as per-row masks (not LEFT, DIAG); rows from the
 // strip's last down to its first. Chains that meet stay merged, so after 4 and after 16 rows the
@@ -1204,18 +1249,66 @@ __global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
     __shared__ int cur[kTbK];
     __shared__ uint16_t map[kTbK], tmp[kTbK];
     __shared__ int wsum[16];
+    __shared__ int sst[4];
     const int s = blockIdx.x;
     const StripDesc sd = a.strips[s];
     const int p = uniform(sd.pair);
-    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 2) return;  // (not pending)
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p])) return;  // (a pair without groups: walk_rw_kernel's)
     const PairDesc pd = a.pairs[p];
     const int n = uniform((int)pd.text_len);
-    const int32_t *st = a.start + kTbStartWords * p;
-    const int i0 = uniform(st[kTbI0]), bs = uniform(st[kTbBs]), ra = uniform(st[kTbRa]);
     const int b = s - uniform(pd.first_strip);
+    int32_t *st = a.start + kTbStartWords * p;
+    int i0, ra, xa, dr, dx;
+    if (a.round == 1)
+    {
+        // every block finds the start cell itself; strip 0's block records it (TbStart), the pair's
+        // state (tb_flag 2: pending, 1: the sequential walk) and the local end strip
+        if (threadIdx.x < kWave)
+        {
+            int i, j, H;
+            const bool ok = tb_pair_start(a, p, pd, threadIdx.x, i, j, H);
+            if (threadIdx.x == 0)
+            {
+                sst[0] = i;
+                sst[1] = j;
+                sst[3] = ok;
+                if (b == 0)
+                {
+                    a.tb_flag[p] = ok ? 2 : 1;
+                    st[kTbI0] = i;
+                    st[kTbJ0] = j;
+                    st[kTbH] = H;
+                    st[kTbBs] = (i - 1) >> 6;
+                    st[kTbRa] = i;  // the first round's line: through (m, n) and (0, 0) / slope 1 from the best cell
+                    st[kTbXa] = j;
+                    st[kTbDr] = a.local ? 1 : i;
+                    st[kTbDx] = a.local ? 1 : j;
+                    st[kTbGres] = -1;
+                    st[kTbBmin] = 0;
+                    a.pend[p] = -1;
+                }
+            }
+        }
+        __syncthreads();
+        if (!sst[3]) return;
+        i0 = ra = sst[0];
+        xa = sst[1];
+        dr = a.local ? 1 : i0;
+        dx = a.local ? 1 : xa;
+    }
+    else
+    {
+        if (uniform(a.tb_flag[p]) != 2) return;  // (resolved or fallen back)
+        i0 = uniform(st[kTbI0]);
+        ra = uniform(st[kTbRa]);
+        xa = uniform(st[kTbXa]);
+        dr = uniform(st[kTbDr]);
+        dx = uniform(st[kTbDx]);
+    }
+    const int bs = (i0 - 1) >> 6;
     if (b > (ra - 1) >> 6) return;  // (below the anchor: resolved, or below the start cell)
     const int kTop = b == bs ? (i0 - 1) & 63 : 63;
-    const int lo = tb_window_lo(b, n, i0, ra, uniform(st[kTbXa]), uniform(st[kTbDr]), uniform(st[kTbDx]));
+    const int lo = tb_window_lo(b, n, i0, ra, xa, dr, dx);
     if (threadIdx.x == 0) a.win[s] = lo;
     if (a.dbg && threadIdx.x == 0) a.dbg[12 * (size_t)s] = __builtin_amdgcn_s_memrealtime();
     const uint32_t *sb = a.masks + uniform64(sd.mask_off) * 4;
@@ -1299,49 +1392,6 @@ __device__ __forceinline__ void tb_stage_tables(int32_t *dst, const int32_t *src
     for (int e = threadIdx.x; e < nt * (kTbK / 4); e += blockDim.x) d4[e] = s4[e];
 }
 
-// One wave per pair: the start cell (global: (m, n); local: the best cell, from the strips' keys as
-// walk_start), the strip holding it, the first round's anchor; tb_flag = 2 (pending), or 1 for the
-// pairs of the sequential walk (no groups, or a local pair without a positive cell: its empty
-// alignment)
-__global__ __launch_bounds__(kWave) void tb_start_kernel(TbArgs a)
-{
-    const int p = blockIdx.x, lane = threadIdx.x;
-    const int g0 = uniform(a.pair_g0[p]), g1 = uniform(a.pair_g0[p + 1]);
-    const PairDesc pd = a.pairs[p];
-    int i = (int)pd.pattern_len, j = (int)pd.text_len, H = 0;
-    bool ok = g1 > g0;
-    if (ok && a.local)
-    {
-        const int first = uniform(pd.first_strip), nstrips = uniform(pd.num_strips);
-        uint64_t k = 0;
-        for (int s = lane; s < nstrips; s += kWave) k = max(k, a.strip_best[first + s]);
-        k = wave_max_u64(k);
-        const int rb = a.key_rowbits;
-        const uint64_t km = (1ull << rb) - 1;
-        H = (int)(k >> (2 * rb));
-        i = (int)(km - ((k >> rb) & km));
-        j = (int)(km - (k & km));
-        ok = H > 0;
-    }
-    else if (ok)
-        H = a.pair_score[p];
-    if (lane != 0) return;
-    a.tb_flag[p] = ok ? 2 : 1;
-    if (!ok) return;
-    int32_t *st = a.start + kTbStartWords * p;
-    st[kTbI0] = i;
-    st[kTbJ0] = j;
-    st[kTbH] = H;
-    st[kTbBs] = (i - 1) >> 6;
-    st[kTbRa] = i;  // the first round's line: through (m, n) and (0, 0) / slope 1 from the best cell
-    st[kTbXa] = j;
-    st[kTbDr] = a.local ? 1 : i;
-    st[kTbDx] = a.local ? 1 : j;
-    st[kTbGres] = -1;
-    st[kTbBmin] = 0;
-    a.pend[p] = -1;
-}
-
 // The group's strips walked from the start: s_lo .. min(s_hi, the start cell's strip); false if none
 __device__ __forceinline__ bool tb_group_span(const TbArgs &a, const TbGroup &g, const PairDesc &pd, int &sLo, int &sHi)
 {
@@ -1388,17 +1438,18 @@ __global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
 __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
 {
     __shared__ int32_t tl[kTbG * kTbK];
+    __shared__ int glo[kTbG];
     __shared__ int xs, gfail, xfail;
     const int p = blockIdx.x;
-    if (uniform(a.tb_flag[p]) != 2) return;
+    // (tb_flag is defined only for pairs with groups: tb_table_kernel writes it)
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p]) || uniform(a.tb_flag[p]) != 2) return;
     const int g0 = uniform(a.pair_g0[p]);
     const PairDesc pd = a.pairs[p];
     const int first = uniform(pd.first_strip);
     int32_t *st = a.start + kTbStartWords * p;
     const int i0 = uniform(st[kTbI0]), bs = uniform(st[kTbBs]);
     // the start cell's group, and the round's first group: the anchor's, or the start cell's
-    int gstart = uniform(a.pair_g0[p + 1]) - 1;
-    while (gstart > g0 && uniform(a.groups[gstart].s_lo) > first + bs) --gstart;
+    const int gstart = g0 + bs / kTbG;  // (a pair's groups are its strips kTbG at a time from strip 0)
     const int gs = uniform(st[kTbGres]) >= 0 ? uniform(st[kTbGres]) : gstart;
     if (threadIdx.x == 0)
     {
@@ -1411,13 +1462,14 @@ __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
         __syncthreads();  // (the previous chunk's lookups are done)
         if (uniform(gfail) >= 0) break;
         tb_stage_tables(tl, a.gtbl, gl, gh - gl);
+        if (threadIdx.x < gh - gl) glo[threadIdx.x] = a.win[min(a.groups[gl + threadIdx.x].s_hi, first + bs)];
         __syncthreads();
         if (threadIdx.x == 0)
         {
             int x = xs;
             for (int g = gh - 1; g >= gl; --g)
             {
-                const int lo = a.win[min(a.groups[g].s_hi, first + bs)];
+                const int lo = glo[g - gl];
                 const int y = (x >= lo && x < lo + kTbK) ? tl[(g - gl) * kTbK + x - lo] : -1;
                 if (y < 0)
                 {
@@ -1483,7 +1535,7 @@ __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
 __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
 {
     __shared__ int32_t tl[kTbG * kTbK];
-    __shared__ int ent[kTbG];
+    __shared__ int ent[kTbG], wlo[kTbG];
     const TbGroup g = a.groups[blockIdx.x];
     const int p = uniform(g.pair);
     if (uniform(a.tb_flag[p]) != 0) return;
@@ -1494,6 +1546,7 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
     const int i0 = uniform(a.start[kTbStartWords * p + kTbI0]), bs = uniform(a.start[kTbStartWords * p + kTbBs]);
     if (sLo < first + uniform(a.start[kTbStartWords * p + kTbBmin])) return;  // (local: not resolved)
     tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
+    if (threadIdx.x <= sHi - sLo) wlo[threadIdx.x] = a.win[sLo + threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0)
     {
@@ -1501,7 +1554,7 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
         for (int s = sHi; s >= sLo; --s)
         {
             ent[sHi - s] = x;
-            x = tl[(s - sLo) * kTbK + x - a.win[s]];
+            x = tl[(s - sLo) * kTbK + x - wlo[s - sLo]];
         }
     }
     __syncthreads();
@@ -1586,31 +1639,44 @@ __global__ __launch_bounds__(kWave) void tb_check_kernel(TbArgs a)
     atomicMax(&a.pend[p], b);
 }
 
-// Local, one thread per pair: the head from the end strip (the highest strip with an end: the first in
-// walk order); a pair without one (never: row 1 always ends the walk) goes to walk_rw_kernel
-__global__ __launch_bounds__(kWave) void tb_finish_kernel(TbArgs a)
+// One block of two waves per pair with groups, last: local, the head from the end strip (the highest
+// strip with an end: the first in walk order); then the pairs the tables left (tb_flag 1, or a local
+// walk without an end among the resolved strips) are walked sequentially (walk_rw_pair)
+template <bool LOCAL>
+__global__ __launch_bounds__(2 * kWave) void tb_finish_kernel(TbArgs a, WalkArgs w)
 {
+    __shared__ RwLds<LOCAL> S;
     const int p = blockIdx.x;
-    if (threadIdx.x != 0 || a.pair_g0[p + 1] == a.pair_g0[p] || a.tb_flag[p] != 0) return;
-    const int b = a.pend[p];
-    if (b < 0)
+    if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p])) return;  // (walk_rw_kernel's)
+    int flag = uniform(a.tb_flag[p]);
+    if (LOCAL && flag == 0)
     {
-        a.tb_flag[p] = 1;
-        return;
+        const int b = uniform(a.pend[p]);
+        if (b >= 0)
+        {
+            if (threadIdx.x == 0)
+            {
+                const int s = a.pairs[p].first_strip + b;
+                const int32_t *st = a.start + kTbStartWords * p;
+                TbHead h;
+                h.kind = kRecRows;
+                h.tail_op = kLeft;
+                h.nrec = a.send[4 * s];
+                h.tail = a.send[4 * s + 1];
+                h.start_text = a.send[4 * s + 2];
+                h.start_pattern = a.send[4 * s + 3];
+                h.pad = 0;
+                h.score = st[kTbH];
+                h.i0 = st[kTbI0];
+                h.j0 = st[kTbJ0];
+                a.heads[p] = h;
+            }
+            return;
+        }
+        flag = 1;
     }
-    const int s = a.pairs[p].first_strip + b;
-    TbHead h;
-    h.kind = kRecRows;
-    h.tail_op = kLeft;
-    h.nrec = a.send[4 * s];
-    h.tail = a.send[4 * s + 1];
-    h.start_text = a.send[4 * s + 2];
-    h.start_pattern = a.send[4 * s + 3];
-    h.pad = 0;
-    h.score = a.start[kTbStartWords * p + kTbH];
-    h.i0 = a.start[kTbStartWords * p + kTbI0];
-    h.j0 = a.start[kTbStartWords * p + kTbJ0];
-    a.heads[p] = h;
+    if (flag == 0 || a.strict) return;  // (global: tb_resolve_kernel wrote the head)
+    walk_rw_pair<LOCAL>(w, p, S);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1877,12 +1943,12 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
     else launch_walk_m<false>(R, a, np, st);
 }
 
-void launch_tb(const TbArgs &args, int nstrips, int ngroups, int np, int rounds, hipStream_t st)
+void launch_tb(const TbArgs &args, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, hipStream_t st)
 {
     TbArgs a = args;
-    hipLaunchKernelGGL(tb_start_kernel, dim3(np), dim3(kWave), 0, st, a);
     for (int r = 1; r <= rounds; ++r)
     {
+        a.round = r;
         a.last_round = r == rounds;
         hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(kTbThreads), 0, st, a);
         hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
@@ -1892,8 +1958,10 @@ void launch_tb(const TbArgs &args, int nstrips, int ngroups, int np, int rounds,
     if (a.local)
     {
         hipLaunchKernelGGL(tb_check_kernel, dim3(nstrips), dim3(kWave), 0, st, a);
-        hipLaunchKernelGGL(tb_finish_kernel, dim3(np), dim3(kWave), 0, st, a);
+        hipLaunchKernelGGL(tb_finish_kernel<true>, dim3(np), dim3(2 * kWave), 0, st, a, w);
     }
+    else
+        hipLaunchKernelGGL(tb_finish_kernel<false>, dim3(np), dim3(2 * kWave), 0, st, a, w);
 }
 
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st)
