@@ -67,6 +67,7 @@ def summarize(tl, n, W, t0=None):
         "cus_used": int(len(set(zip(xcc.tolist(), se.tolist(), cu.tolist())))),
         "max_strips_on_one_simd_concurrently": max_overlap(xcc, se, cu, (hw >> 4) & 3, fed, end),
         "ns_per_step_by_wave_in_group": [round(float(step_ns[w::W].mean()), 2) for w in range(W)],
+        "simd_by_wave_in_group": [sorted(set(((hw[w::W] >> 4) & 3).tolist())) for w in range(W)],
         # cross-group hand-offs whose two groups ran on the same XCD / on different XCDs
         "lag_ns_cross_same_xcd": round(float(lag[cross & (xcc[1:] == xcc[:-1])].mean()), 1) if (cross & (xcc[1:] == xcc[:-1])).any() else None,
         "lag_ns_cross_other_xcd": round(float(lag[cross & (xcc[1:] != xcc[:-1])].mean()), 1) if (cross & (xcc[1:] != xcc[:-1])).any() else None,
