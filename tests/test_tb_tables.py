@@ -72,6 +72,32 @@ print("TB_OK" if not bad else "TB_BAD %r" % (bad,))
 '''
 
 
+SWEEP = r'''
+import os, sys, json, numpy as np
+sys.path[:0] = [sys.argv[1] + "/sequence-alignment-gpu_amd/python", sys.argv[1] + "/oracle"]
+import oracle
+from sa_amd import engine, synthetic
+S4 = synthetic.blast_matrix()
+B50 = np.array(json.load(open(sys.argv[1] + "/tests/golden/matrices.json"))["blosum50"], np.int32).reshape(23, 23)
+rng = np.random.default_rng(int(sys.argv[2]))
+bad = []
+for k in range(24):
+    mode = int(rng.integers(0, 2))
+    prot = bool(rng.integers(0, 4) == 0)
+    A, S = (20, B50) if prot else (4, S4)
+    m = int(rng.integers(512, 3000))
+    n = int(rng.integers(300, 3200))
+    gap = int(rng.choice([5, 5, 3, 0, -1, -2]))
+    t = synthetic.random_sequence(5000 + k, n, A)
+    p = synthetic.mutate(t, 5100 + k, A, m) if rng.integers(0, 2) else synthetic.random_sequence(5200 + k, m, A)
+    r = engine.align_pair(mode, t, p, S, gap, device=0)
+    r.pop("fill_us")
+    if r != oracle.align(mode, t, p, S, gap):
+        bad.append((k, mode, A, n, m, gap))
+print("TB_OK" if not bad else "TB_BAD %r" % (bad,))
+'''
+
+
 def _run(which, **env):
     e = dict(os.environ, **env)
     out = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, which], env=e, capture_output=True, text=True, timeout=110)
@@ -100,3 +126,15 @@ def test_table_traceback_fallback_vs_oracle():
 @pytest.mark.gpu
 def test_sequential_walk_same_pairs_vs_oracle():
     _run("fallback", SA_TB_TABLES="0")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rounds", ["1", "4"])
+def test_table_traceback_random_sweep_vs_oracle(rounds):
+    """24 random pairs (512..3000 rows, 300..3200 columns, both modes, DNA / BLOSUM50, gaps 5 / 3 / 0 /
+    -1 / -2, related or not) with one or four rounds of tables: every result equals the oracle's
+    (pairs the tables leave fall back)."""
+    e = dict(os.environ, SA_TB_ROUNDS=rounds)
+    out = subprocess.run([sys.executable, "-c", SWEEP, ROOT, "7" + rounds], env=e, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert "TB_OK" in out.stdout, out.stdout[-2000:]
