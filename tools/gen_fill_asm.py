@@ -55,6 +55,10 @@ PF_STEP = int(os.environ.get("SA_GEN_PF_STEP", "14"))
 # a 44-clock step leaves two steps too little time for the LDS read (the R = 1 score steps of round 3
 # measured 1 % faster after step 10 than after 14, profiles/r03/dual_dev/pf_timeline.log)
 BAND_PF_STEP = int(os.environ.get("SA_GEN_BAND_PF_STEP", "10"))
+# timing ablations of the strips' feed (experiment builds only, results wrong): "noread" replaces the
+# feed read by a value that passes the tag check, "nocheck" keeps the read and its wait but reports
+# every lane good
+EXP_FEED = os.environ.get("SA_GEN_EXP_FEED", "")
 
 
 def block(local: bool, hn: bool, hp: bool, half: int) -> str:
@@ -82,7 +86,10 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
         sd = f"dst_sel:BYTE_{byte} dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:DWORD"
         qd, qr, dg, fp = regs[k % 4], regs[(k - 1) % 4], regs[(k - 2) % 4], regs[(k - 3) % 4]
         if hp and q == PF_STEP:
-            out.append(f"ds_read_b32 {PF}, {PFA}")
+            if EXP_FEED == "noread":
+                out.append(f"v_not_b32 {PF}, {CTAG}")
+            else:
+                out.append(f"ds_read_b32 {PF}, {PFA}")
         if hn:
             out.append(f"v_mov_b32_dpp {qd}, {qr} wave_shl:1 row_mask:0xf bank_mask:0xf")
         else:
@@ -106,7 +113,11 @@ def block(local: bool, hn: bool, hp: bool, half: int) -> str:
             # the path from the best cell's score, sa_walk.hip local_check)
             if k % 2 == 1:
                 out.append(f"v_max3_i32 {BM}, {BM}, {KEY}, {KEY2}")
-    if hp:
+    if hp and EXP_FEED == "nocheck":
+        out.append("s_waitcnt lgkmcnt(0)")
+        out.append(f"v_bitop3_b32 {PF}, {PF}, {CTAG}, {MSB} bitop3:0xd2")
+        out.append(f"s_mov_b64 {BAD}, 0")
+    elif hp:
         out.append("s_waitcnt lgkmcnt(0)")  # the feed read (issued 4 steps ago) is there
         # tag check: x = entry ^ expected tag (the value when it matches; bitop3 0xD2 = a ^ (~b & c)),
         # bad lanes = x < 0 among the body's U feed lanes; the publish below stands between the

@@ -158,6 +158,8 @@ def main():
                                             enumerate(("feed_slow", "feed_spins", "pub_slow", "pub_spins",
                                                        "feed_slow_past_4096", "feed_spins_past_4096"))}
         rec["feed_slow_by_wave_in_group"] = [round(float(sc[w::W, 0].mean()), 1) for w in range(W)]
+        rec["feed_slow_past_4096_by_wave_in_group"] = [round(float(sc[w::W, 4].mean()), 1) for w in range(W)]
+        rec["feed_spins_past_4096_by_wave_in_group"] = [round(float(sc[w::W, 5].mean()), 1) for w in range(W)]
     print(json.dumps(rec))
     b.close()
 
