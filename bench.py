@@ -60,7 +60,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rows", type=int, default=0, help="rows of the CPU baseline sample (default: full)")
     ap.add_argument("--batch-pipeline", type=int, default=1,
-                    help="batch, one rank: overlap step k's traceback with step k+1's fill (two plan copies)")
+                    help="batch: overlap step k's traceback and result gather with step k+1's fill (two plan copies)")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="batch, one GPU: run rank 0's shard of an N-rank deal (pairs i = 0 mod N) with the step "
+                         "structure of an N-rank run (the strong-scaling curve, modelled per rank on one GPU)")
     ap.add_argument("--batch-chunks", type=int, default=1,
                     help="batch: plans per rank; chunk k's traceback overlaps chunk k+1's fill")
     ap.add_argument("--dry-run", action="store_true",
@@ -187,11 +190,13 @@ class Chunked:
         if two:
             self.s_fill.wait_stream(self.s_tb)
 
-    def copy_results(self, buf) -> None:
-        """Every plan's sa_result array, device to device, into the rows of buf (a (k, 4) int64 tensor)."""
+    def copy_results(self, buf, stream=None) -> None:
+        """Every plan's sa_result array, device to device, into the rows of buf (a (k, 4) int64 tensor),
+        on `stream` (default: the fill stream)."""
         row = 0
+        st = (stream or self.s_fill).cuda_stream
         for j in self.jobs:
-            j.plan.copy_results(buf.data_ptr() + 32 * row, self.s_fill.cuda_stream)
+            j.plan.copy_results(buf.data_ptr() + 32 * row, st)
             row += j.plan.num_pairs
 
     def results(self) -> np.ndarray:
@@ -212,13 +217,16 @@ class Pipelined:
     fill. Every step still fills, traces back and returns all of its pairs (the VALU-bound fill and
     the gather-bound traceback share the CUs)."""
 
-    def __init__(self, a: Chunked, b: Chunked, torch, local):
+    def __init__(self, a: Chunked, b: Chunked, torch, local, gather=None):
         self.sets, self.torch = [a, b], torch
         self.s_fill = torch.cuda.current_stream(local)
         self.s_tb = torch.cuda.Stream(local)
         self.fill_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.tb_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.k, self.pending = 0, None
+        # N ranks: gather(chunked) moves the pending step's results to rank 0 (copy_results + RCCL
+        # gather), issued on the traceback stream so it overlaps the next step's fill as well
+        self.gather = gather
 
     def step(self, ev=None) -> None:
         i = self.k % 2
@@ -243,6 +251,11 @@ class Pipelined:
     def drain(self) -> None:
         """The pending step's results to the host (waits for its traceback only)."""
         if self.pending is None:
+            return
+        if self.gather is not None:
+            with self.torch.cuda.stream(self.s_tb):
+                self.gather(self.sets[self.pending])
+            self.pending = None
             return
         res = np.concatenate([j.plan.results_array(self.s_tb.cuda_stream) for j in self.sets[self.pending].jobs])
         if len(res) and res["status"].any():
@@ -393,7 +406,12 @@ def main():
                     "parallelism": f"replicas{world}"}
     else:
         npairs, L = 4096, 2048
-        mine = distributed.shard(npairs, world, rank)
+        if args.shard_of > 1 and world > 1:
+            raise SystemExit("--shard-of models one rank of an N-rank run on one GPU: run it with --gpus 1")
+        # --shard-of N: rank 0's shard of an N-rank deal, on this one GPU (the per-rank step of the
+        # strong-scaling curve; the RCCL gather of an N-rank run is not in it)
+        deal = args.shard_of if args.shard_of > 1 else world
+        mine = distributed.shard(npairs, deal, rank)
         texts = [synthetic.random_sequence(1000 + 2 * i, L, 4) for i in mine]
         pats = [synthetic.random_sequence(1001 + 2 * i, L, 4) for i in mine]
         # even chunk sizes (the pair-packed fill takes pairs two at a time)
@@ -402,12 +420,19 @@ def main():
         chunks = [DeviceBatch(0, S, gap, texts[a:b], pats[a:b], device=local, rows_per_lane=args.rows_per_lane)
                   for a, b in zip(cuts, cuts[1:]) if b > a]
         job = Chunked(chunks, torch, local)
-        pipe = None
-        if args.batch_pipeline and world == 1 and len(chunks) == 1:
-            twin = Chunked([DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)], torch, local)
-            pipe = Pipelined(job, twin, torch, local)
         # the rank's sa_result rows go device to device into this buffer and on to rank 0 (RCCL gather)
         gbuf = torch.full(((npairs + world - 1) // world, 4), -1, dtype=torch.int64, device=torch.device("cuda", local))
+
+        def gather_pending(ch: Chunked) -> None:
+            ch.copy_results(gbuf, torch.cuda.current_stream(local))
+            distributed.gather_device(gbuf, npairs, world, rank)
+
+        pipe = None
+        if args.batch_pipeline and len(chunks) == 1:
+            # the same two-deep step at every world size: N ranks gather the pending step's results
+            # to rank 0 on the traceback stream, one rank brings them to its host
+            twin = Chunked([DeviceBatch(0, S, gap, texts, pats, device=local, rows_per_lane=args.rows_per_lane)], torch, local)
+            pipe = Pipelined(job, twin, torch, local, gather=gather_pending if world > 1 else None)
         cells_rank = len(mine) * L * L
         pairs_rank = len(mine)
         workload = {"workload": f"dna_global_batch_{npairs}x{L}x{L}", "pairs_total": npairs, "text_len": L,
@@ -415,6 +440,9 @@ def main():
                     "chunks_per_gpu": len(chunks),
                     "step_overlap": ("two-deep: step k's traceback and results overlap step k+1's fill "
                                      "(two plan copies)") if pipe is not None else "none"}
+        if args.shard_of > 1:
+            workload.update(workload=f"dna_global_batch_{npairs}x{L}x{L}_shard_of_{deal}", pairs_total=npairs,
+                            parallelism=f"rank0_of_pairs_sharded{deal} (modelled on one GPU)")
     if not isinstance(job, Chunked):
         job = Chunked([job], torch, local)
     info = job.info()
@@ -541,6 +569,12 @@ def main():
             "direction_bytes_physical_per_launch": info["mask_bytes"],
             "sample_result": {"pair0_score": scores[0] if scores else None, "pairs_per_gpu": pairs_rank},
         }
+        if args.workload == "batch" and args.shard_of > 1:
+            # one rank's step of an N-rank run, measured alone on one GPU: N ranks would finish the
+            # 4096 pairs in about this step time (plus the 16-128 KiB RCCL gather, not measured here)
+            out["shard_model"] = {"shard_of": args.shard_of, "pairs_this_rank": pairs_rank,
+                                  "modelled_n_gpu_gcups": round(value * args.shard_of, 3),
+                                  "note": "modelled, not measured on N GPUs: rank 0's shard on one GPU"}
         if world == 1 and not args.no_cpu_baseline:
             if args.workload == "batch":
                 # the batch is independent pairs: the CPU baseline is every core of this GPU's host

@@ -159,13 +159,21 @@ int sa_plan_fetch_all(sa_plan *plan, sa_result *results, char *text_buf, char *p
 /* Introspection for benches and tests. */
 int sa_plan_info(const sa_plan *plan, int64_t *num_strips, int32_t *rows_per_lane,
                  uint64_t *device_bytes, uint64_t *mask_bytes);
+/* Which fill kernel sa_plan_fill launches for the plan (benches and tests). */
+enum {
+    SA_FILL_STRIPS = 0,      /* one wave per strip (fill_kernel; chains hand rows off in LDS / granules) */
+    SA_FILL_BAND = 1,        /* band fill: 128-row score strips feeding the 64-row strips (R = 1) */
+    SA_FILL_PAIR = 2,        /* pair-packed lone strips: two pairs per wave (fill_pair_kernel) */
+    SA_FILL_PAIR_CHAIN = 3   /* pair-packed chains: a couple of pairs per workgroup, a wave per strip */
+};
+int sa_plan_fill_kind(const sa_plan *plan);
 /* Verification: synchronise `stream` and decode pair `index`'s direction bit-planes into the
  * reference's (pattern_len+1) x (text_len+1) byte DIRECTION matrix (LEFT=0, DIAG=1, TOP=2, STOP=3;
  * row 0 / column 0 as the reference fill sets them, alignSequenceCPU.cpp:145-164, :232-248), so the
  * fill can be compared byte-for-byte with the reference's M. Local plans with one row per lane
- * (rows_per_lane 1) hold no STOP bit: their interior cells decode to the reference's decision before
- * its STOP override (alignSequenceCPU.cpp:181-189; the reference's STOP cells are those whose score
- * is 0, which the traceback recomputes). M_out must hold (m+1)*(n+1) bytes. */
+ * (rows_per_lane 1) hold no STOP bit in their planes (the raw decisions): STOP is put back wherever
+ * the cell's score is 0 (alignSequenceCPU.cpp:188-190), recomputed here on the host from the last
+ * fill's inputs, so every plan returns the reference's M. M_out must hold (m+1)*(n+1) bytes. */
 int sa_plan_fetch_directions(sa_plan *plan, int64_t index, uint8_t *M_out, void *stream);
 
 /* Device pointer to the per-pair sa_result array written by sa_plan_traceback. */

@@ -324,6 +324,7 @@ struct sa_plan {
     // table traceback (sa_walk.h TbArgs; R = 1 plans with a pair of kTbMinStrips strips or more)
     std::vector<TbGroup> tb_groups;
     std::vector<int32_t> tb_pg;  // [np + 1] first group of each pair
+    int64_t tb_slots = 0;        // strip tables (the strips of pairs with groups)
     TbGroup *d_tbgroups = nullptr;
     int32_t *d_tbpg = nullptr, *d_tbl = nullptr, *d_gtbl = nullptr, *d_gent = nullptr, *d_tbflag = nullptr, *d_win = nullptr;
     int32_t *d_tbstart = nullptr, *d_sent = nullptr, *d_sdelta = nullptr, *d_send = nullptr, *d_pend = nullptr;
@@ -346,7 +347,30 @@ struct sa_plan {
 
 namespace {
 
-int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
+// Whether the pairs can run pair-packed (fill_pair_kernel / fill_pair_chain_kernel), whatever R:
+// global, an even number of pairs of one shape, a DNA-sized alphabet, every S + 2g in [0, 255] and
+// every shifted-domain value within u16 (65534 at most: chains mark unpublished LDS entries with
+// 0xffffffff, see sa_fill.hip)
+bool pair_packable(const sa_params *P, const sa_pair *pairs, int64_t np)
+{
+    const int A = P->alphabet_size;
+    const int64_t g = P->gap_penalty;
+    if (P->mode != SA_GLOBAL || np < 2 || np % 2 != 0 || A > 4 || g <= 0 || knobs().no_pair16) return false;
+    int64_t smaxp = 0;
+    for (int e = 0; e < A * A; ++e)
+    {
+        const int64_t v = P->score_matrix[e] + 2 * g;
+        if (v < 0 || v > 255) return false;
+        smaxp = std::max(smaxp, v);
+    }
+    for (int64_t p = 0; p < np; ++p)
+        if (pairs[p].text_len != pairs[0].text_len || pairs[p].pattern_len != pairs[0].pattern_len)
+            return false;
+    const uint64_t n = pairs[0].text_len, m = pairs[0].pattern_len;
+    return n > 0 && m > 0 && (uint64_t)smaxp * std::min(n, m) <= 65534;
+}
+
+int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np, int num_cu)
 {
     int R = P->rows_per_lane;
     if (knobs().rows_per_lane) R = knobs().rows_per_lane;
@@ -361,6 +385,18 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np)
         const int rmax = P->mode == SA_LOCAL ? 16 : 32;
         int r = 1;
         while (r < rmax && (uint64_t)kWave * r < mmax) r <<= 1;
+        if (pair_packable(P, pairs, np))
+        {
+            // size the plan to the GPU: a couple of pairs is one wave per strip, and a batch with
+            // fewer waves than two per SIMD (a shard of the batch on one of N GPUs) leaves SIMDs
+            // idle, its time set by one wave's n + 64 steps of R rows. Shorter strips chained in LDS
+            // (fill_pair_chain_kernel) split each couple over 2 .. 8 waves: R halves (down to 8)
+            // while the waves stay below two per SIMD.
+            const int64_t target = 2 * 4 * (int64_t)std::max(1, num_cu);
+            auto waves = [&](int rr) { return (np / 2) * (int64_t)((mmax + kWave * rr - 1) / (kWave * rr)); };
+            while (r > 8 && waves(r) < target && (int64_t)((mmax + kWave * (r / 2) - 1) / (kWave * (r / 2))) <= kPairChainMax)
+                r >>= 1;
+        }
         return r;
     }
     // few long pairs: the shortest strips keep the wavefront deepest (one row per lane)
@@ -673,7 +709,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
     pl->mode = P->mode;
     pl->A = A;
     pl->gap = (int)g;
-    pl->R = choose_R(P, pairs, np);
+    pl->R = choose_R(P, pairs, np, knobs().max_cus > 0 ? std::min(device_cus(device), knobs().max_cus) : device_cus(device));
     pl->U = (16 / pl->R) > 4 ? 16 / pl->R : 4;
     pl->key_bits = std::min(12, std::max(4, 30 - bitlen(hmax_local)));
     pl->key_rowbits = key_rowbits;
@@ -718,7 +754,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         // kArr8: code_len bytes per copy (4A copies); kArr: A arrays of code_len dwords; else one
         d.code_len = (kPad + d.text_len + 4 * kPad + 3) / 4 * 4;
         // (a possible pair-packed plan, decided below, needs two column profiles per column)
-        const bool maybePair = P->mode == SA_GLOBAL && R >= 16 && A <= 4;
+        const bool maybePair = P->mode == SA_GLOBAL && R >= 8 && A <= 4;
         code_bytes += pl->sk == kArr8 ? (uint64_t)A * d.code_len : pl->sk == kArr ? (uint64_t)A * d.code_len
                                                                                 : (maybePair ? 2 : 1) * d.code_len;
         d.out_off = outb;
@@ -753,26 +789,21 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
     pl->W = choose_W(pl->pairs);
     for (const PairDesc &d : pl->pairs) pl->chain = pl->chain || d.num_strips > 1;
     {
-        // pair-packed fill (fill_pair_kernel): global, lone strips of one shape, DNA-sized alphabet,
-        // every S + 2g in [0, 255] and every value within u16 (see process_pair)
-        bool pair = P->mode == SA_GLOBAL && !pl->chain && np >= 2 && np % 2 == 0 && A <= 4 && R >= 16 &&
-                    g > 0 && !knobs().no_pair16;
-        int64_t smaxp = 0;
-        for (int e = 0; e < A * A; ++e)
+        // pair-packed fill: global, pairs of one shape, DNA-sized alphabet, every S + 2g in [0, 255]
+        // and every value within u16 (see process_pair). Lone strips: fill_pair_kernel; chains of up
+        // to kPairChainMax strips per pair (every pair the same count): fill_pair_chain_kernel, one
+        // workgroup per couple, its LDS rows within a CU's
+        bool pair = R >= 8 && pair_packable(P, pairs, np);
+        if (pair && pl->chain)
         {
-            const int64_t v = P->score_matrix[e] + off2;
-            if (v < 0 || v > 255) pair = false;
-            smaxp = std::max(smaxp, v);
+            const int S = pl->pairs[0].num_strips;
+            pair = S <= kPairChainMax && (size_t)(S - 1) * pair_row_entries((int)pl->pairs[0].text_len) * 4 <= 160 * 1024;
         }
-        for (int64_t p = 0; p < np && pair; ++p)
+        if (pair)
         {
-            const PairDesc &d = pl->pairs[p];
-            if (d.text_len != pl->pairs[0].text_len || d.pattern_len != pl->pairs[0].pattern_len || d.num_strips != 1)
-                pair = false;
-            else if ((uint64_t)smaxp * std::min(d.text_len, d.pattern_len) > 65535)
-                pair = false;
+            pl->sk = kPair;
+            granules = 0;  // (the chains hand their rows off in LDS: no granules)
         }
-        if (pair) pl->sk = kPair;
     }
     // the band fill (sa_fill.hip process_band): R = 1 chains with int8 text profiles (global, or local
     // with g >= 0, which kArr8 implies), W even (a group boundary inside a pair must fall on a band
@@ -861,8 +892,11 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             const PairDesc &d = pl->pairs[p];
             pl->tb_pg[p] = (int32_t)pl->tb_groups.size();
             if (d.num_strips < kTbMinStrips || d.text_len == 0) continue;
+            // strip tables only for the strips of pairs with groups (slot tbl0 + s - s_lo)
             for (int s = 0; s < d.num_strips; s += kTbG)
-                pl->tb_groups.push_back({(int32_t)p, d.first_strip + s, d.first_strip + std::min(d.num_strips, s + kTbG) - 1, 0});
+                pl->tb_groups.push_back({(int32_t)p, d.first_strip + s, d.first_strip + std::min(d.num_strips, s + kTbG) - 1,
+                                         (int32_t)pl->tb_slots + s});
+            pl->tb_slots += d.num_strips;
         }
         pl->tb_pg[np] = (int32_t)pl->tb_groups.size();
         if (pl->tb_groups.empty()) pl->tb_pg.clear();
@@ -900,7 +934,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_score, sizeof(int32_t) * npp},
         {(void **)&pl->d_rec, 4 * recw + 16},
         {(void **)&pl->d_heads, sizeof(TbHead) * npp},
-        {(void **)&pl->d_tbl, ntg ? sizeof(int32_t) * kTbK * nstr : 0},
+        {(void **)&pl->d_tbl, ntg ? sizeof(int32_t) * kTbK * pl->tb_slots : 0},
         {(void **)&pl->d_gtbl, sizeof(int32_t) * kTbK * ntg},
         {(void **)&pl->d_gent, sizeof(int32_t) * ntg},
         {(void **)&pl->d_tbflag, ntg ? sizeof(int32_t) * npp : 0},
@@ -1062,6 +1096,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.num_bands = 0;
         a.num_band_groups = 0;
         a.band_wgs = 0;
+        a.pair_text_len = 0;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;
@@ -1085,7 +1120,14 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             a.num_groups = (units + W - 1) / W;
             grid = std::min(a.num_groups, std::max(1, pl->num_cu) * std::max(1, 8 / W));
         }
-        if (pl->chain_solo)
+        if (pl->sk == kPair && pl->chain)
+        {
+            // pair-packed chains: one workgroup per couple of pairs, one wave per strip of the couple
+            a.num_groups = ns / 2 / pl->pairs[0].num_strips;
+            a.pair_text_len = (int32_t)pl->pairs[0].text_len;
+            grid = a.num_groups;
+        }
+        else if (pl->chain_solo)
         {
             // (plan_create) an LDS request above half a CU's keeps a second workgroup off the CU
             a.chain_lds = std::max(a.chain_lds, 96 * 1024);
@@ -1111,7 +1153,8 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
                 grid = a.band_wgs + std::max(1, std::min(a.num_groups, pl->num_cu - a.band_wgs));
             }
         }
-        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, W, pl->chain, st);
+        launch_fill(pl->R, a, pl->mode == SA_LOCAL, pl->sk, grid, pl->sk == kPair && pl->chain ? pl->pairs[0].num_strips : W,
+                    pl->chain, st);
         HIP_TRY(hipGetLastError());
         if (tlPath)
         {
@@ -1373,6 +1416,37 @@ int sa_plan_fetch_directions(sa_plan *pl, int64_t index, uint8_t *M, void *strea
             M[i * cols + j] = (uint8_t)(pl->mode == SA_GLOBAL || R == 1 ? (b0 ? 1u : (b1 ? 2u : 0u)) : (b0 | (b1 << 1)));
         }
     }
+    if (local && R == 1)
+    {
+        // local R = 1 planes hold the raw decisions (the walk recovers STOP from H along the path):
+        // the reference's M has STOP wherever best <= 0, i.e. H == 0 (alignSequenceCPU.cpp:175-190),
+        // so H is recomputed here row by row from the fill's inputs and those cells are overwritten
+        if (!pl->filled || !pl->d_text_in || !pl->d_pattern_in)
+            return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: the plan has not been filled");
+        std::vector<int8_t> tx(n), px(m);
+        HIP_TRY(hipMemcpyAsync(tx.data(), pl->d_text_in + pd.text_off, n, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(px.data(), pl->d_pattern_in + pd.pattern_off, m, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (int8_t c : tx)
+            if (c < 0 || c >= pl->A) return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: text letter outside the alphabet");
+        for (int8_t c : px)
+            if (c < 0 || c >= pl->A) return fail(SA_ERR_INVALID, "sa_plan_fetch_directions: pattern letter outside the alphabet");
+        const int64_t g = pl->gap;
+        std::vector<int64_t> prev(cols, 0), cur(cols, 0);
+        for (uint64_t i = 1; i <= m; ++i)
+        {
+            cur[0] = 0;
+            const int32_t *srow = &pl->h_table[(size_t)px[i - 1] * pl->A];  // S + g (local table)
+            for (uint64_t j = 1; j <= n; ++j)
+            {
+                const int64_t d = prev[j - 1] + srow[tx[j - 1]] - g, l = cur[j - 1] - g, u = prev[j] - g;
+                const int64_t best = std::max(d, std::max(l, u));
+                cur[j] = best > 0 ? best : 0;
+                if (best <= 0) M[i * cols + j] = 3;
+            }
+            std::swap(prev, cur);
+        }
+    }
     return SA_OK;
 }
 
@@ -1385,6 +1459,13 @@ int sa_plan_info(const sa_plan *pl, int64_t *num_strips, int32_t *rows_per_lane,
     if (device_bytes) *device_bytes = pl->bytes_total;
     if (mask_bytes) *mask_bytes = pl->bytes_masks;
     return SA_OK;
+}
+
+int sa_plan_fill_kind(const sa_plan *pl)
+{
+    if (!pl) return fail(SA_ERR_INVALID, "sa_plan_fill_kind: null plan");
+    if (pl->sk == kPair) return pl->chain ? SA_FILL_PAIR_CHAIN : SA_FILL_PAIR;
+    return pl->band ? SA_FILL_BAND : SA_FILL_STRIPS;
 }
 
 const void *sa_plan_device_results(const sa_plan *pl) { return pl ? (const void *)pl->d_results : nullptr; }

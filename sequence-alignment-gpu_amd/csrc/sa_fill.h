@@ -41,12 +41,19 @@ struct FillArgs {
     int32_t num_bands;
     int32_t num_band_groups;    // ceil(num_bands / W)
     int32_t band_wgs;
+    int32_t pair_text_len;      // pair-packed chains (fill_pair_chain_kernel): the pairs' common text length
 };
 
 constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..37: experiment progress stamps)
 constexpr int kMaxWaves = 4;       // compute waves per chain workgroup (+1 I/O wave: 320 threads; one
                                    // compute wave per SIMD: two per SIMD ran 2.2x slower per step)
 constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed batch kernel
+constexpr int kPairChainMax = 8;   // strips per pair (waves per workgroup) of a pair-packed chain
+constexpr int kPairFeedOff = 64;   // LDS row entry of column c: c + kPairFeedOff (c >= -63)
+// (entries: columns -63 .. n + 2U published, and every lane of a consumer's feed read up to column
+// nSteps + 63 <= n + 2U + 126)
+__host__ __device__ constexpr int pair_row_entries(int n) { return (n + kPairFeedOff + 4 * kWave + 63) / 64 * 64; }
+
 
 // Where a strip's substitution scores come from (SK). Every table already holds S + 2g (global) or
 // S + g (local), the offsets the recurrences below fold in:
@@ -59,7 +66,8 @@ constexpr int kPairWaves = 4;      // waves per workgroup of the pair-packed bat
 //           per letter so that every lane's 16-byte load is dword aligned (lane k reads copy k%4);
 //           one global_load_dwordx4 serves a whole 16-step body and the byte is picked by the
 //           add itself (SDWA src1_sel:BYTE_q, sign-extended).
-//   kPair   pair-packed lone strips (fill_pair_kernel): per column the two pairs' column profiles.
+//   kPair   pair-packed strips (fill_pair_kernel; chains: fill_pair_chain_kernel): per column the
+//           two pairs' column profiles.
 // The zero padding of the profiles keeps the ramp cells left of column 1 at the boundary value.
 enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3, kPair = 4 };
 template <int SK>

@@ -1234,19 +1234,28 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as16(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
 __device__ __forceinline__ uint32_t as32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 
-template <int R>
-__device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane)
+// CHAINS of pair-packed strips (pairs taller than one strip, fill_pair_chain_kernel): one workgroup
+// per couple of pairs, one wave per strip of the couple (the same strip of both pairs, packed as
+// above); a strip's bottom row goes to the strip below through an LDS array of the whole row (n + a
+// wave's skew entries: no wrap, no laps), filled with 0xffffffff at the workgroup's start. Both
+// halves of a published value are at most 65534 (plan_create's bound), so that word is never a
+// value: the consumer's U feed entries are ready when none of them is 0xffffffff. No global memory
+// and no other workgroup is involved, so the chain cannot deadlock whatever the residency. This sizes
+// a batch's plan to the GPU when it has few pairs (a shard of the batch on one of N GPUs): strips of
+// 8 or 16 rows per lane give the couple 2-4 waves instead of one.
+template <int R, bool HP, bool HN>
+__device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int sB, int lane, lds_int *feed, lds_int *pub)
 {
     constexpr int U = Cfg<R>::U;
     constexpr int SB = Cfg<R>::SB;      // slots per body (per pair)
     constexpr int NP = SB / 16;         // packed words per plane per body
     constexpr int NW = Cfg<R>::NW, LW = Cfg<R>::LW;
-    static_assert(R >= 16 && Cfg<R>::BPC == 1 && SB % 32 == 0, "pair kernel: R >= 16, a body is one chunk");
-    const StripDesc dA = a.strips[sA], dB = a.strips[sA + 1];
+    static_assert(R >= 8 && Cfg<R>::BPC == 1 && SB % 32 == 0, "pair kernel: R >= 8, a body is one chunk");
+    const StripDesc dA = a.strips[sA], dB = a.strips[sB];
     const PairDesc pA = a.pairs[dA.pair], pB = a.pairs[dB.pair];
     const int n = (int)pA.text_len, m = (int)pA.pattern_len;
     const int g = a.gap;
-    const int rowTop = 1 + lane * R;
+    const int rowTop = dA.row0 + lane * R;
     uint32_t rsel[R];
     sfor<R>([&](auto Rc) {
         constexpr int rho = decltype(Rc)::value;
@@ -1264,6 +1273,7 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
     sfor<R>([&](auto Rc) { F[decltype(Rc)::value] = 0; });
     uint32_t upPrev = 0;
     int Q;
+    uint32_t P = 0;  // HN: the bottom row's queue (lane 63 enters a value per step)
     int TA[2 * U], TB[2 * U];
     auto load_codes = [&](int s0, int (&dst)[2 * U]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(8)));
@@ -1282,7 +1292,21 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
         const int s1 = s0 + U;
         load_codes(s1, Tn);
         uint32_t acc[2][NP];
-        asm volatile("v_mov_b32 %0, 0" : "=v"(Q));  // row 0 boundary (opaque zero: see feed())
+        if constexpr (HP)
+        {
+            // lane q < U: the strip above's bottom row at column s0 + 1 + q (lane 0 enters column
+            // s0 + 1 + q at step s0 + q); columns past n are never published and never needed
+            lds_int *f = feed + (s0 + 1 + kPairFeedOff) + lane;
+            const bool need = lane < U && s0 + 1 + lane <= n;
+            Q = lds_ld(f);
+            while (__builtin_amdgcn_ballot_w64(need && Q == -1) != 0)
+            {
+                __builtin_amdgcn_s_sleep(1);
+                Q = lds_ld(f);
+            }
+        }
+        else asm volatile("v_mov_b32 %0, 0" : "=v"(Q));  // row 0 boundary (opaque zero: see feed())
+        uint32_t x0[U * R], x1[U * R];
         sfor<U>([&](auto Qc) {
             constexpr int q = decltype(Qc)::value;
             const int Qn = __builtin_amdgcn_mov_dpp(Q, 0x130, 0xf, 0xf, true);  // wave_shl:1
@@ -1297,33 +1321,34 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
                 act = (c >= 0) && (c < n);
             }
             const uint32_t colA = (uint32_t)T[2 * q], colB = (uint32_t)T[2 * q + 1];
-            uint32_t x0[R], x1[R];
             sfor<R>([&](auto Rc) {
                 constexpr int rho = decltype(Rc)::value;
+                constexpr int e = q * R + rho;  // the body's slot
                 const uint32_t sc = __builtin_amdgcn_perm(colB, colA, rsel[rho]);
                 const u16x2 D = as16(diag) + as16(sc);
                 const uint32_t left = F[rho];
                 const u16x2 M = __builtin_elementwise_max(as16(left), as16(up));
                 uint32_t Fn = as32(__builtin_elementwise_max(D, M));
-                x0[rho] = as32(M - D);                     // DIAG iff sign
-                x1[rho] = as32(as16(left) - as16(up));     // up > left iff sign
+                x0[e] = as32(M - D);                     // DIAG iff sign
+                x1[e] = as32(as16(left) - as16(up));     // up > left iff sign
                 if constexpr (RAMP) Fn = act ? Fn : left;
                 diag = left;
                 up = Fn;
                 F[rho] = Fn;
-                // rows rho-8 and rho of a 16-row group are slots s and s+8 of packed word w: insert
-                // as soon as both exist (keeps at most 8 rows of differences live)
+                // slots e - 8 and e of a 16-slot group (rows rho - 8 and rho of this step for R >= 16,
+                // row rho of the step before and of this one for R = 8): insert as soon as both exist
+                // (keeps at most 8 slots of differences live)
                 // perm selectors 8..11 replicate the sign bit of a 16-bit half over a whole byte, so
                 // the four signs arrive as 0x00 / 0xff bytes and one bit-field insert puts them at
                 // 7 - sl of each byte, no shift: 2 VALU per 4 bits. Slot sl = 0 keeps the whole bytes;
                 // slots 1..7 overwrite their low bits.
-                if constexpr (rho % 16 >= 8)
+                if constexpr (e % 16 >= 8)
                 {
-                    constexpr int sl = rho % 16 - 8;
-                    constexpr int w = (q * R + rho) / 16;
+                    constexpr int sl = e % 16 - 8;
+                    constexpr int w = e / 16;
                     constexpr uint32_t mask = (0x80808080u >> sl);
-                    const uint32_t y0 = __builtin_amdgcn_perm(x0[rho - 8], x0[rho], 0x0b090a08u);
-                    const uint32_t y1 = __builtin_amdgcn_perm(x1[rho - 8], x1[rho], 0x0b090a08u);
+                    const uint32_t y0 = __builtin_amdgcn_perm(x0[e - 8], x0[e], 0x0b090a08u);
+                    const uint32_t y1 = __builtin_amdgcn_perm(x1[e - 8], x1[e], 0x0b090a08u);
                     if constexpr (sl == 0)
                     {
                         acc[0][w] = y0;
@@ -1336,7 +1361,15 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
                     }
                 }
             });
+            // HN: lane 63's bottom row (column s0 + q - 62) enters the publish queue
+            if constexpr (HN) P = (uint32_t)__builtin_amdgcn_update_dpp((int)F[R - 1], (int)P, 0x130, 0xf, 0xf, false);
         });
+        if constexpr (HN)
+        {
+            // lanes 64 - U .. 63 hold columns s0 - 62 .. s0 + U - 63 (ramp columns <= 0 land below
+            // the entries of column 1 and are never read)
+            if (lane >= kWave - U) lds_st(pub + (s0 + lane + U - 126 + kPairFeedOff), (int)P);
+        }
         // split the packed words into each pair's 32-slot words: {plane 0 words, plane 1 words}
         const int chunk = (s1 * R) / Cfg<R>::CS - 1;
         uint32_t vA[LW], vB[LW];
@@ -1357,7 +1390,7 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
         });
     };
     // tail pairs of bodies from the first pair holding a body with s1 > n (the global score row is
-    // in every lone strip)
+    // in every strip that holds row m)
     const int sTail = max(0, n / (2 * U) * (2 * U));
     int s0 = 0;
     for (; s0 < sTail; s0 += 2 * U)
@@ -1370,8 +1403,8 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int lane
         body(std::true_type{}, s0, TA, TB);
         body(std::true_type{}, s0 + U, TB, TA);
     }
-    const int rm = m - 1;  // strip-relative row of the last DP row
-    if (lane == rm / R)
+    const int rm = m - dA.row0;  // strip-relative row of the last DP row
+    if (!HN && rm >= 0 && rm < kWave * R && lane == rm / R)
     {
         uint32_t v = F[0];
         sfor<R>([&](auto Rc) {
@@ -1400,8 +1433,30 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
         const int grp = uniform(unit);
         if (grp * W >= units) break;
         const int u = grp * W + w;
-        if (u < units) process_pair<R>(a, 2 * u, lane);
+        if (u < units) process_pair<R, false, false>(a, 2 * u, 2 * u + 1, lane, nullptr, nullptr);
     }
+}
+
+// Chains: workgroup u = pairs 2u and 2u + 1 (every pair has blockDim / 64 strips), wave w = strip w of
+// both; dynamic LDS = (strips - 1) rows of pair_row_entries(n) entries.
+template <int R>
+__global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(FillArgs a)
+{
+    extern __shared__ int prowRaw[];
+    lds_int *prow = (lds_int *)prowRaw;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = uniform((int)(threadIdx.x / kWave));
+    const int S = (int)(blockDim.x / kWave);
+    const int u = (int)blockIdx.x;
+    const PairDesc pA = a.pairs[2 * u], pB = a.pairs[2 * u + 1];
+    const int E = pair_row_entries((int)pA.text_len);
+    for (int e = threadIdx.x; e < (S - 1) * E; e += blockDim.x) lds_st(prow + e, -1);
+    __syncthreads();
+    const int sA = uniform(pA.first_strip) + w, sB = uniform(pB.first_strip) + w;
+    lds_int *feed = prow + (w - 1) * E, *pub = prow + w * E;
+    if (w == 0) process_pair<R, false, true>(a, sA, sB, lane, feed, pub);
+    else if (w + 1 < S) process_pair<R, true, true>(a, sA, sB, lane, feed, pub);
+    else process_pair<R, true, false>(a, sA, sB, lane, feed, pub);
 }
 
 // The I/O wave of a group: global granules of the previous group's last strip -> ring[0], and
@@ -1760,8 +1815,19 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
     }
     else if (sk == kPair)
     {
-        if constexpr (R >= 16)
-            hipLaunchKernelGGL(fill_pair_kernel<R>, dim3(grid), dim3(kWave * W), 0, st, a);
+        if constexpr (R >= 8)
+        {
+            if (chain)
+            {
+                // pair-packed chains: grid = couples, W = strips per pair, one LDS row per strip boundary
+                const size_t lds = (size_t)(W - 1) * pair_row_entries(a.pair_text_len) * 4;
+                if (lds > 65536)
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_pair_chain_kernel<R>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                hipLaunchKernelGGL(fill_pair_chain_kernel<R>, dim3(grid), dim3(kWave * W), lds, st, a);
+            }
+            else hipLaunchKernelGGL(fill_pair_kernel<R>, dim3(grid), dim3(kWave * W), 0, st, a);
+        }
     }
     else if (local)
     {

@@ -27,7 +27,7 @@ struct TbHead {
     int32_t kind;     // kRecRows / kRecCols
     int32_t tail_op;  // kLeft / kTop
     int32_t score;
-    int32_t pad;
+    int32_t err;      // nonzero: the walk gave up on a spin bound (the pair's status becomes SA_ERR_TIMEOUT)
     int64_t start_text, start_pattern;  // Response::startInAlignedText / Pattern
 };
 
@@ -84,7 +84,9 @@ enum TbStart {
     kTbStartWords = 12
 };
 struct TbGroup {
-    int32_t pair, s_lo, s_hi, pad;  // the plan's strip indices, s_lo <= s_hi (one pair's)
+    int32_t pair, s_lo, s_hi;  // the plan's strip indices, s_lo <= s_hi (one pair's)
+    int32_t tbl0;              // strip s_lo's table slot (tables exist only for pairs with groups:
+                               // slot of strip s = tbl0 + s - s_lo)
 };
 struct TbArgs {
     const StripDesc *strips;

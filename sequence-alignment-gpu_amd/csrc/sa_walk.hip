@@ -420,7 +420,7 @@ __device__ __forceinline__ bool walk_start(const WalkArgs &a, int p, int n, int 
     h.tail_op = kLeft;
     h.tail = 0;
     h.nrec = 0;
-    h.pad = 0;
+    h.err = 0;
     if constexpr (!LOCAL)
     {
         h.score = nstrips > 0 ? a.pair_score[p] : -a.gap * (n + m);
@@ -837,12 +837,19 @@ __device__ __forceinline__ void walk_rw_pair(const WalkArgs &a, const int p, RwL
                 // and the header are there when the sequence word is
                 ++chkSeq;
                 // (the stager takes no checks once the walk has ended: stop waiting for the slot then)
-                bool over = false;
+                bool over = false, lost = false;
                 for (uint32_t spin = 1; uniform(((volatile int *)chkCtl)[1]) < chkSeq - 2; ++spin)
                 {
                     if ((over = uniform(((volatile int *)chkCtl)[3]) != 0)) break;
                     if (spin > 16) __builtin_amdgcn_s_sleep(1);
-                    if (spin > (1u << 26)) break;  // (never: the stager always takes or ends; a bound, not a wait)
+                    // (never: the stager always takes or ends; a bound, not a wait. Exhausted, the slot
+                    // is not posted and the pair fails loudly: h.err -> SA_ERR_TIMEOUT)
+                    if ((lost = spin > (1u << 26))) break;
+                }
+                if (lost)
+                {
+                    h.err = 1;
+                    break;
                 }
                 if (over)
                 {
@@ -919,15 +926,27 @@ __device__ __forceinline__ void walk_rw_pair(const WalkArgs &a, const int p, RwL
         {
             // the stager's verdict (the last strip posted is strip 0 at the latest, whose row 1 always
             // ends the walk)
-            for (uint32_t spin = 1; uniform(((volatile int *)chkCtl)[3]) == 0; ++spin)
+            for (uint32_t spin = 1; h.err == 0 && uniform(((volatile int *)chkCtl)[3]) == 0; ++spin)
             {
                 if (spin > 16) __builtin_amdgcn_s_sleep(1);
-                if (spin > (1u << 26)) break;  // (a bound, never reached: strip 0's check always ends the walk)
+                // (a bound, never reached: strip 0's check always ends the walk; exhausted, the
+                // verdict words were never written and the pair fails loudly instead of reading them)
+                if (spin > (1u << 26)) h.err = 1;
             }
-            h.nrec = ((volatile int *)chkCtl)[4];
-            h.tail = ((volatile int *)chkCtl)[5];
-            h.start_text = ((volatile int *)chkCtl)[6];
-            h.start_pattern = ((volatile int *)chkCtl)[7];
+            if (h.err == 0)
+            {
+                h.nrec = ((volatile int *)chkCtl)[4];
+                h.tail = ((volatile int *)chkCtl)[5];
+                h.start_text = ((volatile int *)chkCtl)[6];
+                h.start_pattern = ((volatile int *)chkCtl)[7];
+            }
+            else
+            {
+                h.nrec = 0;
+                h.tail = 0;
+                h.start_text = 0;
+                h.start_pattern = 0;
+            }
         }
     }
     if (lane == 0)
@@ -1374,7 +1393,8 @@ __global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
             stamp[3 + 3 * ph] = (uint64_t)D;
         }
     }
-    int32_t *out = a.tbl + (int64_t)s * kTbK;
+    // (the pair's first group starts at its first strip: table slots are per pair with groups)
+    int32_t *out = a.tbl + (int64_t)(uniform(a.groups[uniform(a.pair_g0[p])].tbl0) + b) * kTbK;
     for (int t = threadIdx.x; t < kTbK; t += blockDim.x) out[t] = lo + t <= n ? cur[map[t]] : -1;
     if (dbg && threadIdx.x == 0)
     {
@@ -1414,7 +1434,7 @@ __global__ __launch_bounds__(1024) void tb_compose_kernel(TbArgs a)
     int sLo, sHi;
     if (!tb_group_span(a, g, pd, sLo, sHi)) return;
     const int n = uniform((int)pd.text_len);
-    tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
+    tb_stage_tables(tl, a.tbl, uniform(g.tbl0) + sLo - uniform(g.s_lo), sHi - sLo + 1);
     if (threadIdx.x <= sHi - sLo) wl[threadIdx.x] = a.win[sLo + threadIdx.x];
     __syncthreads();
     const int loHi = wl[sHi - sLo];
@@ -1519,7 +1539,7 @@ __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
     h.tail_op = kLeft;
     h.tail = xs;  // row 0: LEFT to column 0 (traceBackNW :80-81)
     h.nrec = (int)pd.pattern_len;
-    h.pad = 0;
+    h.err = 0;
     h.score = st[kTbH];
     h.i0 = (int)pd.pattern_len;
     h.j0 = (int)pd.text_len;
@@ -1545,7 +1565,7 @@ __global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
     const int first = uniform(pd.first_strip);
     const int i0 = uniform(a.start[kTbStartWords * p + kTbI0]), bs = uniform(a.start[kTbStartWords * p + kTbBs]);
     if (sLo < first + uniform(a.start[kTbStartWords * p + kTbBmin])) return;  // (local: not resolved)
-    tb_stage_tables(tl, a.tbl, sLo, sHi - sLo + 1);
+    tb_stage_tables(tl, a.tbl, uniform(g.tbl0) + sLo - uniform(g.s_lo), sHi - sLo + 1);
     if (threadIdx.x <= sHi - sLo) wlo[threadIdx.x] = a.win[sLo + threadIdx.x];
     __syncthreads();
     if (threadIdx.x == 0)
@@ -1665,7 +1685,7 @@ __global__ __launch_bounds__(2 * kWave) void tb_finish_kernel(TbArgs a, WalkArgs
                 h.tail = a.send[4 * s + 1];
                 h.start_text = a.send[4 * s + 2];
                 h.start_pattern = a.send[4 * s + 3];
-                h.pad = 0;
+                h.err = 0;
                 h.score = st[kTbH];
                 h.i0 = st[kTbI0];
                 h.j0 = st[kTbJ0];
@@ -1912,7 +1932,7 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
         // the control word of this fill: a pair aligned after a hand-off timeout or on bad input carries
         // the error itself, so a device-to-device copy of the results (sa_plan_copy_results, the RCCL
         // gather) keeps it
-        r.status = a.ctrl->abort_flag ? SA_ERR_TIMEOUT : (a.ctrl->bad_input ? SA_ERR_INVALID : SA_OK);
+        r.status = a.ctrl->abort_flag || h.err ? SA_ERR_TIMEOUT : (a.ctrl->bad_input ? SA_ERR_INVALID : SA_OK);
         r.num_alignment_bytes = (uint64_t)L;
         r.start_text = (uint64_t)h.start_text;
         r.start_pattern = (uint64_t)h.start_pattern;

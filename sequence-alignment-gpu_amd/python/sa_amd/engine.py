@@ -17,12 +17,15 @@ SA_GLOBAL, SA_LOCAL = 0, 1
 STATUS = {0: "SA_OK", 1: "SA_ERR_INVALID", 2: "SA_ERR_NOMEM", 3: "SA_ERR_HIP", 4: "SA_ERR_UNSUPPORTED",
           5: "SA_ERR_TIMEOUT"}
 
+# sa_plan_fill_kind (include/sa_hip.h SA_FILL_*)
+FILL_KINDS = {0: "strips", 1: "band", 2: "pair", 3: "pair_chain"}
+
 # Symbols declared in include/sa_hip.h (checked by tests/test_capi.py).
 EXPORTS = ("sa_align_pair", "sa_plan_create", "sa_plan_destroy", "sa_plan_fill", "sa_plan_traceback",
            "sa_plan_fetch_results", "sa_plan_fetch_alignment", "sa_plan_info", "sa_plan_device_results", "sa_plan_copy_results",
            "sa_device_count", "sa_last_error", "sa_abi_version", "sa_selftest", "sa_plan_fetch_directions", "sa_release_workspace",
            "sa_plan_output_bytes", "sa_plan_fetch_all", "sa_align_batch", "sa_batch_deal", "sa_build_id",
-           "sa_batch_last_stats")
+           "sa_batch_last_stats", "sa_plan_fill_kind")
 
 
 class SaParams(ctypes.Structure):
@@ -70,6 +73,8 @@ def _load():
     L.sa_plan_info.argtypes = [P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(U64), ctypes.POINTER(U64)]
     L.sa_plan_fetch_directions.argtypes = [P, ctypes.c_int64, P, P]
+    L.sa_plan_fill_kind.argtypes = [P]
+    L.sa_plan_fill_kind.restype = I
     L.sa_plan_device_results.argtypes = [P]
     L.sa_plan_device_results.restype = P
     L.sa_plan_copy_results.argtypes = [P, P, P]
@@ -227,7 +232,9 @@ class Plan:
     def info(self) -> dict:
         ns, r, db, mb = ctypes.c_int64(), ctypes.c_int32(), ctypes.c_uint64(), ctypes.c_uint64()
         _check(lib.sa_plan_info(self.handle, ctypes.byref(ns), ctypes.byref(r), ctypes.byref(db), ctypes.byref(mb)))
-        return {"num_strips": ns.value, "rows_per_lane": r.value, "device_bytes": db.value, "mask_bytes": mb.value}
+        kind = lib.sa_plan_fill_kind(self.handle)
+        return {"num_strips": ns.value, "rows_per_lane": r.value, "device_bytes": db.value, "mask_bytes": mb.value,
+                "fill_kernel": FILL_KINDS.get(kind, kind)}
 
     def fill(self, d_text: int, d_pattern: int, stream: int | None = None) -> None:
         _check(lib.sa_plan_fill(self.handle, d_text, d_pattern, stream))

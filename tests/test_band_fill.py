@@ -36,7 +36,7 @@ def check(mode, n, m, gap, seed, related, S=S):
     got = b.directions(0)
     b.close()
     exp = np.empty((m + 1) * (n + 1), np.uint8)
-    oracle.fill_only(2 if mode == 1 else 0, t, p, S, gap, exp)  # (local R = 1: raw decisions, no STOP)
+    oracle.fill_only(mode, t, p, S, gap, exp)  # (the reference's M, STOP included)
     nbad = int((got != exp).sum())
     if nbad:
         bad.append(("dirs", mode, n, m, gap, nbad))

@@ -67,10 +67,12 @@ def test_fixture_matches_large_json_and_oracle(golden):
             assert record(got) == doc[name]["records"][i], (name, i)
 
 
-def _check_batch(name: str, count: int):
+def _check_batch(name: str, count: int, every: int = 1):
+    """Pairs 0, every, 2 * every, ... below count * every (every = N: rank 0's shard of an N-rank deal)."""
     from sa_amd.batch import DeviceBatch
     doc = fixture()
-    pairs = [inputs(name, i) for i in range(count)]
+    idx = list(range(0, count * every, every))
+    pairs = [inputs(name, i) for i in idx]
     b = DeviceBatch(doc[name]["mode"], synthetic.blast_matrix(), doc["gap"], [t for t, _ in pairs],
                     [p for _, p in pairs])
     b.fill()
@@ -78,7 +80,7 @@ def _check_batch(name: str, count: int):
     got = b.all_alignments()
     info = b.plan.info()
     b.close()
-    bad = [i for i in range(count) if record(got[i]) != doc[name]["records"][i]]
+    bad = [i for k, i in enumerate(idx) if record(got[k]) != doc[name]["records"][i]]
     assert not bad, f"{len(bad)} of {count} {name} pairs differ, first {bad[:5]}"
     return info
 
@@ -88,6 +90,16 @@ def test_config5_every_pair(eng):
     """The 4096-pair plan bench.py times, every pair bit-exact vs the reference."""
     info = _check_batch("global", 4096)
     assert info["num_strips"] == 4096 and info["rows_per_lane"] == 32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [2, 4, 8])
+def test_config5_shard_every_pair(eng, shards):
+    """Rank 0's shard of config 5 on an N-rank deal (pairs i = 0 mod N: 2048 / 1024 / 512 pairs), the
+    plan bench.py --shard-of N times: the planner sizes it to the GPU (pair-packed chains of shorter
+    strips once one strip per pair leaves SIMDs idle), every pair bit-exact vs the reference."""
+    info = _check_batch("global", 4096 // shards, every=shards)
+    assert info["fill_kernel"] in ("pair", "pair_chain") and info["rows_per_lane"] >= 8
 
 
 @pytest.mark.gpu

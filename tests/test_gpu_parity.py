@@ -201,9 +201,8 @@ def test_batch_plan_config5(eng, golden):
 def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane, gap):
     """The fill alone, cell by cell: the engine's DIRECTION matrix (decoded from its bit-planes) equals
     the reference's (m+1)x(n+1) byte matrix M (alignSequenceCPU.cpp:116-284) on every cell. Local
-    plans with one row per lane store no STOP bit: every interior cell is compared with the
-    reference's decision before its STOP override (:181-189; oracle mode 2), and the STOP cells -- the
-    cells whose score is 0 -- are the traceback's (the alignment tests)."""
+    plans with one row per lane store no STOP bit in their planes (the raw decisions); the decoder
+    puts STOP back wherever H is 0 (:188-190), so every plan returns the reference's own M."""
     from sa_amd.batch import DeviceBatch
     S = synthetic.blast_matrix()
     for k, (n, m) in enumerate([(1500, 1400), (700, 700), (130, 66)]):
@@ -213,7 +212,7 @@ def test_fill_direction_matrix_vs_oracle(eng, mode, rows_per_lane, gap):
         b.fill()
         got = b.directions(0)
         exp = np.empty((m + 1) * (n + 1), np.uint8)
-        oracle.fill_only(2 if mode == 1 and rows_per_lane == 1 else mode, t, p, S, gap, exp)
+        oracle.fill_only(mode, t, p, S, gap, exp)
         bad = int((got != exp).sum())
         b.close()
         assert bad == 0, (n, m, bad)
@@ -232,6 +231,35 @@ def test_pair_packed_fill_vs_oracle(eng, rows_per_lane):
         texts.append(t)
         pats.append(synthetic.mutate(t, 950 + k, 4, m) if k % 2 else synthetic.random_sequence(970 + k, m, 4))
     b = DeviceBatch(0, S, 5, texts, pats, rows_per_lane=rows_per_lane)
+    res = b.run()
+    for k in range(4):
+        got = b.directions(k)
+        exp = np.empty((m + 1) * (n + 1), np.uint8)
+        oracle.fill_only(0, texts[k], pats[k], S, 5, exp)
+        assert int((got != exp).sum()) == 0, k
+        at, ap = b.alignment(k)
+        assert dict(res[k], aligned_text=at, aligned_pattern=ap) == oracle.align(0, texts[k], pats[k], S, 5)
+    b.close()
+
+
+@pytest.mark.parametrize("rows_per_lane,n,m", [(8, 1500, 1100), (16, 1500, 1100), (8, 2100, 1024), (8, 100, 1300),
+                                                (8, 700, 4000), (8, 700, 4200), (16, 3000, 2047)])
+def test_pair_packed_chain_vs_oracle(eng, rows_per_lane, n, m):
+    """Pair-packed CHAINS (fill_pair_chain_kernel): a couple of equal-shape global pairs per workgroup,
+    one wave per strip of both, each strip's bottom row handed to the strip below in LDS. Every
+    pair's DIRECTION matrix, score and alignment equal the oracle's, cell by cell: several strips,
+    a partial last strip, fewer columns than rows, exactly 8 strips (the most a chain takes) and 9
+    (which falls back to the one-wave chained fill)."""
+    from sa_amd.batch import DeviceBatch
+    S = synthetic.blast_matrix()
+    texts, pats = [], []
+    for k in range(4):
+        t = synthetic.random_sequence(2900 + k, n, 4)
+        texts.append(t)
+        pats.append(synthetic.mutate(t, 2950 + k, 4, m) if k % 2 else synthetic.random_sequence(2970 + k, m, 4))
+    b = DeviceBatch(0, S, 5, texts, pats, rows_per_lane=rows_per_lane)
+    strips = -(-m // (64 * rows_per_lane))
+    assert b.plan.info()["fill_kernel"] == ("pair_chain" if strips <= 8 else "strips")
     res = b.run()
     for k in range(4):
         got = b.directions(k)
@@ -284,7 +312,7 @@ def test_chain_ring_laps_across_groups(eng, mode):
     for k in (1, 4):
         n, m = shapes[k]
         exp = np.empty((m + 1) * (n + 1), np.uint8)
-        oracle.fill_only(2 if mode == 1 else 0, texts[k], pats[k], S, 5, exp)  # (local: raw decisions)
+        oracle.fill_only(mode, texts[k], pats[k], S, 5, exp)  # (the reference's M, STOP included)
         assert int((b.directions(k) != exp).sum()) == 0, shapes[k]
     b.close()
 

@@ -138,3 +138,54 @@ def test_table_traceback_random_sweep_vs_oracle(rounds):
     out = subprocess.run([sys.executable, "-c", SWEEP, ROOT, "7" + rounds], env=e, capture_output=True, text=True, timeout=110)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert "TB_OK" in out.stdout, out.stdout[-2000:]
+
+
+LONG_LOCAL = r'''
+import os, sys, json, hashlib, numpy as np
+sys.path[:0] = [sys.argv[1] + "/sequence-alignment-gpu_amd/python"]
+from sa_amd import engine, synthetic
+S = synthetic.blast_matrix()
+# a related local pair past 131072 rows (the default multi-round table path): 6000 unrelated rows, a
+# mutated copy of 140000 text letters, 6000 unrelated rows, so traceBackSW ends (STOP) thousands of
+# rows above row 1 and the walk crosses the round boundary
+t = synthetic.random_sequence(880, 150000, 4)
+core = synthetic.mutate(t[4000:144000], 881, 4, 138000)
+p = np.concatenate([synthetic.random_sequence(882, 6000, 4), core, synthetic.random_sequence(883, 6000, 4)])
+r = engine.align_pair(1, t, p, S, 5, device=0)
+r.pop("fill_us")
+at, ap = r.pop("aligned_text"), r.pop("aligned_pattern")
+alpha = "ATCG"
+sc = 0
+for a, b in zip(at, ap):
+    sc += -5 if a == "-" or b == "-" else int(S[alpha.index(b), alpha.index(a)])
+ft, fp = "".join(alpha[c] for c in t), "".join(alpha[c] for c in p)
+tu, pu = at.replace("-", ""), ap.replace("-", "")
+ok_t = ft.find(tu, max(0, r["start_text"] - 1)) in (r["start_text"], r["start_text"] + 1)
+ok_p = fp.find(pu, max(0, r["start_pattern"] - 1)) in (r["start_pattern"], r["start_pattern"] + 1)
+r["sha"] = hashlib.sha256((at + "|" + ap).encode()).hexdigest()
+r["rescored"] = sc
+r["substrings_at_starts"] = bool(ok_t and ok_p)
+print("RESULT " + json.dumps(r))
+'''
+
+
+@pytest.mark.gpu
+def test_long_local_table_rounds_vs_sequential_walk():
+    """Local table traceback past 131072 rows (the default rounds path, which re-anchors on the path's
+    slope and keeps the groups resolved before a failure): a related 150000 x 150000 local pair whose
+    walk ends (STOP) about 6000 rows above row 1. The oracle would take minutes here, so the default
+    path is compared field by field with the sequential walk (SA_TB_TABLES=0) in a second process, and
+    both alignments must re-score to the score and be substrings of the inputs at the reported starts
+    (traceBackSW's start quirk: the first aligned index or one less, alignSequenceCPU.cpp:45-53)."""
+    res = {}
+    for tag, env in (("tables", {}), ("walk", {"SA_TB_TABLES": "0"})):
+        out = subprocess.run([sys.executable, "-c", LONG_LOCAL, ROOT], env=dict(os.environ, **env),
+                             capture_output=True, text=True, timeout=110)
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+        line = [x for x in out.stdout.splitlines() if x.startswith("RESULT ")]
+        assert line, out.stdout[-2000:]
+        res[tag] = __import__("json").loads(line[-1][7:])
+    a, b = res["tables"], res["walk"]
+    assert a == b, (a, b)
+    assert a["rescored"] == a["score"] and a["substrings_at_starts"], a
+    assert a["start_pattern"] > 4000 and a["num_bytes"] > 131072, a
