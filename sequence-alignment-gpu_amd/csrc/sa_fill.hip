@@ -1383,6 +1383,13 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int sB, 
         });
         uint32_t *dA_ = mkA + (size_t)chunk * (kWave * LW);
         uint32_t *dB_ = mkB + (size_t)chunk * (kWave * LW);
+        if constexpr (LW == 2)
+        {
+            // (R = 8: a chunk is 32 slots, one word per plane per lane)
+            *reinterpret_cast<uint2 *>(dA_) = uint2{vA[0], vA[1]};
+            *reinterpret_cast<uint2 *>(dB_) = uint2{vB[0], vB[1]};
+        }
+        static_assert(LW == 2 || LW % 4 == 0, "chunk store");
         sfor<LW / 4>([&](auto Xc) {
             constexpr int x = decltype(Xc)::value;
             *reinterpret_cast<u32x4 *>(dA_ + 4 * x) = u32x4{vA[4 * x], vA[4 * x + 1], vA[4 * x + 2], vA[4 * x + 3]};
