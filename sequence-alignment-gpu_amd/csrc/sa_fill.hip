@@ -1473,10 +1473,9 @@ __global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
 // (strips: the launch's strips, or its bands in a band workgroup)
 __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *strips, int nstrips, int *cons, int *drain,
-                                        lds_int *rings, int grp, int W, int lane)
+                                        lds_int *rings, int first, int count, int lane)
 {
-    const int first = grp * W;
-    const int last = min(first + W, nstrips) - 1;
+    const int last = min(first + count, nstrips) - 1;
     const StripDesc sf = strips[first];
     const StripDesc sl = strips[last];
     const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
@@ -1723,9 +1722,16 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         __syncthreads();
         const int grp = uniform(H.group);
         if (grp >= ngroups) break;
+        // the group's strips: W from grp * W, or (band fill, FillArgs::group_first) a group of its own size
+        int first = grp * W, count = W;
+        if (!bandRole && a.group_first)
+        {
+            first = uniform(a.group_first[grp]);
+            count = uniform(a.group_first[grp + 1]) - first;
+        }
         if (CHAIN && w == W)
         {
-            io_wave(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane);
+            io_wave(a, strips, nstrips, H.cons, H.drain, rings, first, count, lane);
         }
         else if (CHAIN && w > W)
         {
@@ -1739,8 +1745,8 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         }
         else
         {
-            const int idx = grp * W + w;
-            if (idx < nstrips)
+            const int idx = first + w;
+            if (w < count && idx < nstrips)
             {
                 // the strip kind is compile-time inside process_strip (branch-free body boundaries)
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one

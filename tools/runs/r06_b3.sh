@@ -1,0 +1,23 @@
+# round 6: band fill with tail strip groups of 2 (SA_TAIL_PAIRS, default on): band / parity tests, then a
+# same-box A/B against groups of 4 everywhere (SA_TAIL_PAIRS=0), three repetitions, and timelines
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
+  tests/test_band_fill.py tests/test_gpu_parity.py tests/test_tb_tables.py > gpurun_out/r6b3_tests.log 2>&1 || { tail -n 40 gpurun_out/r6b3_tests.log; exit 1; }
+tail -n 1 gpurun_out/r6b3_tests.log
+: > gpurun_out/ab.log
+for rep in 1 2 3; do
+  for tp in 0 1; do
+    SA_TAIL_PAIRS=$tp LABEL=tail$tp timeout -k 10 600 bash tools/ab.sh -w "headline local dna8k protein4k" -s 20 > /dev/null || exit 1
+  done
+done
+cut -c1-160 gpurun_out/ab.log
+for tp in 0 1; do
+  SA_TAIL_PAIRS=$tp timeout -k 10 120 python tools/timeline.py --n 32768 --m 32768 --mode 0 > gpurun_out/r6b3_tl_tail$tp.json 2> gpurun_out/r6b3_tl_err.log || { cat gpurun_out/r6b3_tl_err.log; exit 1; }
+done
+python3 - <<'PY'
+import json
+for tp in (0, 1):
+    d = json.load(open(f"gpurun_out/r6b3_tl_tail{tp}.json"))
+    print("tail", tp, {k: d.get(k) for k in ("total_us", "ns_per_step_mean", "clk_per_step_mean", "lag_ns_in_group_mean", "lag_ns_cross_group_mean")},
+          {k: v for k, v in d.items() if k.startswith("band") and not isinstance(v, (list, dict))})
+PY
