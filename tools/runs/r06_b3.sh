@@ -18,6 +18,8 @@ python3 - <<'PY'
 import json
 for tp in (0, 1):
     d = json.load(open(f"gpurun_out/r6b3_tl_tail{tp}.json"))
-    print("tail", tp, {k: d.get(k) for k in ("total_us", "ns_per_step_mean", "clk_per_step_mean", "lag_ns_in_group_mean", "lag_ns_cross_group_mean")},
-          {k: v for k, v in d.items() if k.startswith("band") and not isinstance(v, (list, dict))})
+    b = d.get("bands", {})
+    print("tail", tp, "strips", {k: d.get(k) for k in ("total_us", "last_start_us", "last_end_us", "ns_per_step_mean", "cus_used")},
+          "bands", {k: b.get(k) for k in ("last_start_us", "last_end_us", "ns_per_step_mean", "lag_ns_in_group_mean", "lag_ns_cross_group_mean")})
+    print("   strip ns/step by strip", d.get("ns_per_step_by_strip"))
 PY
