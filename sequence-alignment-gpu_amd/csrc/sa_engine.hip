@@ -212,6 +212,7 @@ struct Knobs {
     int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
                                     // capacity (default kBandPersistRows*)
     int tail_pairs = 1;             // SA_TAIL_PAIRS=0: band fill strip groups all of W (no tail groups of 2)
+    int pair_prio = 0;              // SA_PAIR_PRIO=1: pair-packed fills issue at priority 2 (s_setprio)
 };
 
 const Knobs &knobs()
@@ -239,6 +240,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_TAIL_PAIRS")) v.tail_pairs = std::atoi(e);
+        if (const char *e = get("SA_PAIR_PRIO")) v.pair_prio = std::atoi(e) != 0;
         return v;
     }();
     return k;
@@ -1154,6 +1156,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.band_wgs = 0;
         a.pair_text_len = 0;
         a.group_first = nullptr;
+        a.pair_prio = knobs().pair_prio;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;

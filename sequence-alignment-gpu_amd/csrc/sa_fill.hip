@@ -1432,6 +1432,7 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
     const int w = uniform((int)(threadIdx.x / kWave));
     const int W = (int)(blockDim.x / kWave);
     const int units = a.num_strips / 2;
+    if (a.pair_prio) __builtin_amdgcn_s_setprio(2);
     while (true)
     {
         __syncthreads();
@@ -1457,6 +1458,7 @@ __global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(
     const int u = (int)blockIdx.x;
     const PairDesc pA = a.pairs[2 * u], pB = a.pairs[2 * u + 1];
     const int E = pair_row_entries((int)pA.text_len);
+    if (a.pair_prio) __builtin_amdgcn_s_setprio(2);
     for (int e = threadIdx.x; e < (S - 1) * E; e += blockDim.x) lds_st(prow + e, -1);
     __syncthreads();
     const int sA = uniform(pA.first_strip) + w, sB = uniform(pB.first_strip) + w;

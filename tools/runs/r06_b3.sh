@@ -23,3 +23,11 @@ for tp in (0, 1):
           "bands", {k: b.get(k) for k in ("last_start_us", "last_end_us", "ns_per_step_mean", "lag_ns_in_group_mean", "lag_ns_cross_group_mean")})
     print("   strip ns/step by strip", d.get("ns_per_step_by_strip"))
 PY
+# the pipelined batch step with the pair-packed fill at issue priority 2 (SA_PAIR_PRIO) vs default
+: > gpurun_out/ab.log
+for rep in 1 2 3; do
+  for pp in 0 1; do
+    SA_PAIR_PRIO=$pp LABEL=prio$pp timeout -k 10 600 bash tools/ab.sh -w "batch" -s 20 > /dev/null || exit 1
+  done
+done
+cut -c1-200 gpurun_out/ab.log
