@@ -3,7 +3,7 @@
 # lane (0 = planner; 16/8/4 forced: pair chains for 16/8, the one-wave chained fill for 4)
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
-  tests/test_gpu_parity.py tests/test_batch_golden.py tests/test_tb_tables.py tests/test_band_fill.py > gpurun_out/r6b2_tests.log 2>&1 || { tail -n 40 gpurun_out/r6b2_tests.log; exit 1; }
+  tests/test_gpu_parity.py tests/test_batch_golden.py tests/test_tb_tables.py tests/test_band_fill.py tests/test_edge_cases.py > gpurun_out/r6b2_tests.log 2>&1 || { tail -n 40 gpurun_out/r6b2_tests.log; exit 1; }
 tail -n 2 gpurun_out/r6b2_tests.log
 for N in 1 2 4 8; do
   for R in 0 32 16 8; do

@@ -1,9 +1,7 @@
 # round 6: band fill with tail strip groups of 2 (SA_TAIL_PAIRS, default on): band / parity tests, then a
 # same-box A/B against groups of 4 everywhere (SA_TAIL_PAIRS=0), three repetitions, and timelines
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
-  tests/test_band_fill.py tests/test_gpu_parity.py tests/test_tb_tables.py > gpurun_out/r6b3_tests.log 2>&1 || { tail -n 40 gpurun_out/r6b3_tests.log; exit 1; }
-tail -n 1 gpurun_out/r6b3_tests.log
+# (the band / parity tests run in r06_b2.sh, which r06_b4.sh runs first)
 : > gpurun_out/ab.log
 for rep in 1 2 3; do
   for tp in 0 1; do
