@@ -213,6 +213,7 @@ struct Knobs {
                                     // capacity (default kBandPersistRows*)
     int tail_pairs = 1;             // SA_TAIL_PAIRS=0: band fill strip groups all of W (no tail groups of 2)
     int pair_prio = 0;              // SA_PAIR_PRIO=1: pair-packed fills issue at priority 2 (s_setprio)
+    int64_t tail_lone = -1;         // SA_TAIL_LONE: lone tail strips of a band fill (default: n / 1100)
 };
 
 const Knobs &knobs()
@@ -241,6 +242,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_TAIL_PAIRS")) v.tail_pairs = std::atoi(e);
         if (const char *e = get("SA_PAIR_PRIO")) v.pair_prio = std::atoi(e) != 0;
+        if (const char *e = get("SA_TAIL_LONE")) v.tail_lone = std::max(0LL, std::atoll(e));
         return v;
     }();
     return k;
@@ -839,43 +841,70 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             // a strip at a group start takes its feed from the granules of the band above, the others
             // from the strip above through the group's rings, and a group's last strip publishes nothing.
             // strip groups: W strips each; with CUs to spare (every group in flight), the latest groups
-            // of the chains split in two. A chain's end is its last strips' n steps, and a strip
-            // sharing its CU with three others steps at 44 clk against 40 beside one other (the bands:
-            // 38), so the tail strips pace closer to the bands that feed them.
-            // Groups start on even strips either way (band boundaries).
+            // of the chains split in two, and the very latest into lone strips. A chain's end is its
+            // last strips' n steps, and a strip sharing its CU with three others steps at 44 clk against
+            // 40 beside one other and 35.5 alone (the bands that feed them: 38), so the tail strips
+            // pace closer to the bands. Groups of 4 and 2 start on even strips (band
+            // boundaries); a lone even strip publishes its bottom row to granules for the lone odd strip
+            // below it (one-wave chain hand-off), a lone odd strip publishes nothing.
+            std::vector<int64_t> firsts;
+            std::vector<char> lone;  // per strip: in a group of one
             {
                 const int64_t ns = (int64_t)pl->strips.size();
-                std::vector<int64_t> firsts;
                 for (int64_t i = 0; i < ns; i += pl->W) firsts.push_back(i);
+                lone.assign(ns, 0);
                 int64_t spare = pl->num_cu - (int64_t)firsts.size() - bandGroups;
                 if (pl->W == 4 && spare > 0 && knobs().tail_pairs != 0 && stripGroups + bandGroups <= pl->num_cu)
                 {
-                    // latest first: by the first strip's offset inside its pair
+                    // latest first: by the first strip's row inside its pair
                     std::vector<int64_t> order;
                     for (size_t g = 0; g < firsts.size(); ++g)
                         if (firsts[g] + 2 < ns) order.push_back((int64_t)g);
-                    auto offset = [&](int64_t g) {
-                        const StripDesc &sd = pl->strips[firsts[g]];
-                        return (int64_t)sd.row0;
-                    };
-                    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) { return offset(x) > offset(y); });
-                    std::vector<char> split(firsts.size(), 0);
+                    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
+                        return pl->strips[firsts[x]].row0 > pl->strips[firsts[y]].row0;
+                    });
+                    // lone strips for the latest ~n/1100 strips of a chain: a strip starts about 53 band
+                    // steps after the one two above it, so over n steps a lone strip (paced by its band)
+                    // gains on a strip in a pair (17.1 vs 16.3 ns per step) what that many strip lags
+                    // cost; groups of 2 for the rest of the spare CUs
+                    int64_t nmax = 0;
+                    for (const PairDesc &d : pl->pairs) nmax = std::max<int64_t>(nmax, (int64_t)d.text_len);
+                    int64_t loneLeft = knobs().tail_lone >= 0 ? knobs().tail_lone : nmax / 1100;
+                    std::vector<int> split(firsts.size(), 0);  // 1: 2 + 2, 2: four lone strips
                     for (int64_t g : order)
                     {
-                        if (spare <= 0) break;
-                        split[g] = 1;
-                        --spare;
+                        const int64_t size = std::min<int64_t>(pl->W, ns - firsts[g]);
+                        if (loneLeft > 0 && size == 4 && spare >= 3)
+                        {
+                            split[g] = 2;
+                            spare -= 3;
+                            loneLeft -= 4;
+                        }
+                        else if (spare >= 1)
+                        {
+                            split[g] = 1;
+                            --spare;
+                        }
+                        else break;
                     }
                     std::vector<int64_t> f2;
                     for (size_t g = 0; g < firsts.size(); ++g)
                     {
                         f2.push_back(firsts[g]);
-                        if (split[g]) f2.push_back(firsts[g] + 2);
+                        if (split[g] == 1) f2.push_back(firsts[g] + 2);
+                        if (split[g] == 2)
+                        {
+                            for (int q = 1; q < 4; ++q) f2.push_back(firsts[g] + q);
+                            for (int q = 0; q < 4; ++q) lone[firsts[g] + q] = 1;
+                        }
                     }
                     firsts.swap(f2);
                     pl->sgroups.assign(firsts.begin(), firsts.end());
                     pl->sgroups.push_back((int32_t)ns);
                 }
+            }
+            {
+                const int64_t ns = (int64_t)pl->strips.size();
                 std::vector<char> gstart(ns + 1, 0), glast(ns + 1, 0);
                 for (size_t g = 0; g < firsts.size(); ++g)
                 {
@@ -888,7 +917,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                 {
                     const uint64_t n = d.text_len;
                     const int B = (d.num_strips + 1) / 2;
-                const int64_t fb = (int64_t)pl->bands.size();
+                    const int64_t fb = (int64_t)pl->bands.size();
                     for (int b = 0; b + 1 < B; ++b)
                     {
                         StripDesc bd = pl->strips[d.first_strip + 2 * b];
@@ -904,9 +933,18 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                     {
                         StripDesc &sd = pl->strips[d.first_strip + k];
                         const int i = d.first_strip + k;
-                        if (k + 1 < d.num_strips && glast[i]) sd.flags &= ~kHasNext;
+                        // a lone even strip feeds the strip below through granules of its own
+                        const bool pub = lone[i] && k % 2 == 0 && k + 1 < d.num_strips;
+                        if (k + 1 < d.num_strips && glast[i] && !pub) sd.flags &= ~kHasNext;
                         sd.bnd_out = 0;
-                        sd.bnd_in = (k > 0 && gstart[i]) ? pl->bands[fb + k / 2 - 1].bnd_out : 0;
+                        if (pub)
+                        {
+                            sd.bnd_out = granules;
+                            granules += n + 8;
+                        }
+                        sd.bnd_in = (k > 0 && gstart[i]) ? (k % 2 == 0 ? pl->bands[fb + k / 2 - 1].bnd_out
+                                                                       : pl->strips[i - 1].bnd_out)
+                                                         : 0;
                     }
                 }
             }
