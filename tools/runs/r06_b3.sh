@@ -9,6 +9,7 @@ for rep in 1 2; do
   LABEL=lone timeout -k 10 600 bash tools/ab.sh -w "headline local dna8k protein4k" -s 20 > /dev/null || exit 1
 done
 cut -c1-160 gpurun_out/ab.log
+cp gpurun_out/ab.log gpurun_out/r6b3_ab_tail.log
 for v in "0 0" "1 0" "1 -1"; do
   set -- $v
   tag=tail$1_$2
@@ -32,3 +33,4 @@ for rep in 1 2 3; do
   done
 done
 cut -c1-200 gpurun_out/ab.log
+cp gpurun_out/ab.log gpurun_out/r6b3_ab_prio.log
