@@ -398,14 +398,17 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np, int num_cu)
         if (pair_packable(P, pairs, np))
         {
             // size the plan to the GPU: a couple of pairs is one wave per strip, and a batch with
-            // fewer waves than two per SIMD (a shard of the batch on one of N GPUs) leaves SIMDs
-            // idle, its time set by one wave's n + 64 steps of R rows. Shorter strips chained in LDS
-            // (fill_pair_chain_kernel) split each couple over 2 .. 8 waves: R halves (down to 8)
-            // while the waves stay below two per SIMD.
-            const int64_t target = 2 * 4 * (int64_t)std::max(1, num_cu);
-            auto waves = [&](int rr) { return (np / 2) * (int64_t)((mmax + kWave * rr - 1) / (kWave * rr)); };
-            while (r > 8 && waves(r) < target && (int64_t)((mmax + kWave * (r / 2) - 1) / (kWave * (r / 2))) <= kPairChainMax)
-                r >>= 1;
+            // fewer waves than SIMDs (a shard of the batch on one of N GPUs) leaves SIMDs idle, its
+            // time set by one wave's n + 64 steps of R rows. Strips of 8 rows per lane chained in LDS
+            // (fill_pair_chain_kernel) split each couple over up to kPairChainMax waves. Measured on
+            // config 5's shards (profiles/r06/shard_sweep_v1.log): 1024 pairs 0.86 ms at R = 8 against
+            // 1.22 at 16 and 1.24 at 32; 512 pairs 0.52 / 0.73 / 1.19; 2048 pairs (one wave per SIMD
+            // at R = 32) 1.44 at 32 against 1.50 at 8 and 1.82 at 16: chains of two R = 16 strips never
+            // pay, so the choice is one strip per pair or R = 8 chains.
+            const int64_t simds = 4 * (int64_t)std::max(1, num_cu);
+            const int64_t strips8 = (int64_t)((mmax + kWave * 8 - 1) / (kWave * 8));
+            if ((np / 2) * (int64_t)((mmax + kWave * r - 1) / (kWave * r)) < simds && r > 8 && strips8 <= kPairChainMax)
+                r = 8;
         }
         return r;
     }
