@@ -214,6 +214,7 @@ struct Knobs {
     int tail_pairs = 1;             // SA_TAIL_PAIRS=0: band fill strip groups all of W (no tail groups of 2)
     int pair_prio = 0;              // SA_PAIR_PRIO=1: pair-packed fills issue at priority 2 (s_setprio)
     int64_t tail_lone = -1;         // SA_TAIL_LONE: lone tail strips of a band fill (default: n / 1100)
+    int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
 };
 
 const Knobs &knobs()
@@ -243,6 +244,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_TAIL_PAIRS")) v.tail_pairs = std::atoi(e);
         if (const char *e = get("SA_PAIR_PRIO")) v.pair_prio = std::atoi(e) != 0;
         if (const char *e = get("SA_TAIL_LONE")) v.tail_lone = std::max(0LL, std::atoll(e));
+        if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
         return v;
     }();
     return k;
@@ -406,9 +408,10 @@ int choose_R(const sa_params *P, const sa_pair *pairs, int64_t np, int num_cu)
             // at R = 32) 1.44 at 32 against 1.50 at 8 and 1.82 at 16: chains of two R = 16 strips never
             // pay, so the choice is one strip per pair or R = 8 chains.
             const int64_t simds = 4 * (int64_t)std::max(1, num_cu);
-            const int64_t strips8 = (int64_t)((mmax + kWave * 8 - 1) / (kWave * 8));
-            if ((np / 2) * (int64_t)((mmax + kWave * r - 1) / (kWave * r)) < simds && r > 8 && strips8 <= kPairChainMax)
-                r = 8;
+            const int rc = knobs().pair_chain_r > 0 ? knobs().pair_chain_r : 8;
+            const int64_t stripsC = (int64_t)((mmax + kWave * rc - 1) / (kWave * rc));
+            if ((np / 2) * (int64_t)((mmax + kWave * r - 1) / (kWave * r)) < simds && r > rc && stripsC <= kPairChainMax)
+                r = rc;
         }
         return r;
     }
@@ -767,7 +770,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         // kArr8: code_len bytes per copy (4A copies); kArr: A arrays of code_len dwords; else one
         d.code_len = (kPad + d.text_len + 4 * kPad + 3) / 4 * 4;
         // (a possible pair-packed plan, decided below, needs two column profiles per column)
-        const bool maybePair = P->mode == SA_GLOBAL && R >= 8 && A <= 4;
+        const bool maybePair = P->mode == SA_GLOBAL && R >= 4 && A <= 4;
         code_bytes += pl->sk == kArr8 ? (uint64_t)A * d.code_len : pl->sk == kArr ? (uint64_t)A * d.code_len
                                                                                 : (maybePair ? 2 : 1) * d.code_len;
         d.out_off = outb;
@@ -806,7 +809,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         // and every value within u16 (see process_pair). Lone strips: fill_pair_kernel; chains of up
         // to kPairChainMax strips per pair (every pair the same count): fill_pair_chain_kernel, one
         // workgroup per couple, its LDS rows within a CU's
-        bool pair = R >= 8 && pair_packable(P, pairs, np);
+        bool pair = R >= 4 && pair_packable(P, pairs, np);
         if (pair && pl->chain)
         {
             const int S = pl->pairs[0].num_strips;

@@ -1246,11 +1246,12 @@ __device__ __forceinline__ uint32_t as32(u16x2 v) { return __builtin_bit_cast(ui
 template <int R, bool HP, bool HN>
 __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int sB, int lane, lds_int *feed, lds_int *pub)
 {
-    constexpr int U = Cfg<R>::U;
-    constexpr int SB = Cfg<R>::SB;      // slots per body (per pair)
+    // a body is one stored chunk (R = 4: 8 steps, two of the plan's 4-step bodies)
+    constexpr int U = Cfg<R>::SB >= 32 ? Cfg<R>::U : 32 / R;
+    constexpr int SB = U * R;           // slots per body (per pair)
     constexpr int NP = SB / 16;         // packed words per plane per body
     constexpr int NW = Cfg<R>::NW, LW = Cfg<R>::LW;
-    static_assert(R >= 8 && Cfg<R>::BPC == 1 && SB % 32 == 0, "pair kernel: R >= 8, a body is one chunk");
+    static_assert(R >= 4 && SB == Cfg<R>::CS, "pair kernel: R >= 4, a body is one chunk");
     const StripDesc dA = a.strips[sA], dB = a.strips[sB];
     const PairDesc pA = a.pairs[dA.pair], pB = a.pairs[dB.pair];
     const int n = (int)pA.text_len, m = (int)pA.pattern_len;
@@ -1408,7 +1409,8 @@ __device__ __forceinline__ void process_pair(const FillArgs &a, int sA, int sB, 
     for (; s0 < nSteps; s0 += 2 * U)
     {
         body(std::true_type{}, s0, TA, TB);
-        body(std::true_type{}, s0 + U, TB, TA);
+        // (R = 4: the strip's steps are a multiple of 8, not always of 16)
+        if (s0 + U < nSteps) body(std::true_type{}, s0 + U, TB, TA);
     }
     const int rm = m - dA.row0;  // strip-relative row of the last DP row
     if (!HN && rm >= 0 && rm < kWave * R && lane == rm / R)
@@ -1830,7 +1832,7 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
     }
     else if (sk == kPair)
     {
-        if constexpr (R >= 8)
+        if constexpr (R >= 4)
         {
             if (chain)
             {

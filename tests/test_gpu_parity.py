@@ -243,7 +243,8 @@ def test_pair_packed_fill_vs_oracle(eng, rows_per_lane):
 
 
 @pytest.mark.parametrize("rows_per_lane,n,m", [(8, 1500, 1100), (16, 1500, 1100), (8, 2100, 1024), (8, 100, 1300),
-                                                (8, 700, 4000), (8, 700, 4200), (16, 3000, 2047)])
+                                                (8, 700, 4000), (8, 700, 4200), (16, 3000, 2047), (4, 1500, 1100),
+                                                (4, 2047, 2048), (4, 333, 2049), (4, 70, 900)])
 def test_pair_packed_chain_vs_oracle(eng, rows_per_lane, n, m):
     """Pair-packed CHAINS (fill_pair_chain_kernel): a couple of equal-shape global pairs per workgroup,
     one wave per strip of both, each strip's bottom row handed to the strip below in LDS. Every
