@@ -67,14 +67,14 @@ def test_fixture_matches_large_json_and_oracle(golden):
             assert record(got) == doc[name]["records"][i], (name, i)
 
 
-def _check_batch(name: str, count: int, every: int = 1):
+def _check_batch(name: str, count: int, every: int = 1, rows_per_lane: int = 0):
     """Pairs 0, every, 2 * every, ... below count * every (every = N: rank 0's shard of an N-rank deal)."""
     from sa_amd.batch import DeviceBatch
     doc = fixture()
     idx = list(range(0, count * every, every))
     pairs = [inputs(name, i) for i in idx]
     b = DeviceBatch(doc[name]["mode"], synthetic.blast_matrix(), doc["gap"], [t for t, _ in pairs],
-                    [p for _, p in pairs])
+                    [p for _, p in pairs], rows_per_lane=rows_per_lane)
     b.fill()
     b.traceback()
     got = b.all_alignments()
@@ -99,7 +99,16 @@ def test_config5_shard_every_pair(eng, shards):
     plan bench.py --shard-of N times: the planner sizes it to the GPU (pair-packed chains of shorter
     strips once one strip per pair leaves SIMDs idle), every pair bit-exact vs the reference."""
     info = _check_batch("global", 4096 // shards, every=shards)
-    assert info["fill_kernel"] in ("pair", "pair_chain") and info["rows_per_lane"] >= 8
+    assert info["fill_kernel"] in ("pair", "pair_chain") and info["rows_per_lane"] >= 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows_per_lane", [4, 8, 16])
+def test_config5_shard_of_8_chain_heights(eng, rows_per_lane):
+    """The 512-pair shard with the pair-packed chains of every strip height the planner can pick
+    (8 / 4 / 2 strips per pair), every pair bit-exact vs the reference."""
+    info = _check_batch("global", 512, every=8, rows_per_lane=rows_per_lane)
+    assert info["fill_kernel"] == "pair_chain" and info["rows_per_lane"] == rows_per_lane
 
 
 @pytest.mark.gpu
