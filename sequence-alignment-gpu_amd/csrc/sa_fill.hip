@@ -1476,10 +1476,15 @@ __global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
 // (strips: the launch's strips, or its bands in a band workgroup)
+// (VG: the group is strips first .. first + count - 1 of a group table, FillArgs::group_first;
+// otherwise strips grp * W .. grp * W + W - 1: that path's code is kept exactly as it was, since the
+// band loop's pace is sensitive to the code around it)
+template <bool VG = false>
 __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *strips, int nstrips, int *cons, int *drain,
-                                        lds_int *rings, int first, int count, int lane)
+                                        lds_int *rings, int grp, int W, int lane, int vgFirst = 0, int vgCount = 0)
 {
-    const int last = min(first + count, nstrips) - 1;
+    const int first = VG ? vgFirst : grp * W;
+    const int last = min(first + (VG ? vgCount : W), nstrips) - 1;
     const StripDesc sf = strips[first];
     const StripDesc sl = strips[last];
     const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
@@ -1667,7 +1672,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false>
+template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false, bool VG = false>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -1726,16 +1731,16 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         __syncthreads();
         const int grp = uniform(H.group);
         if (grp >= ngroups) break;
-        // the group's strips: W from grp * W, or (band fill, FillArgs::group_first) a group of its own size
-        int first = grp * W, count = W;
-        if (!bandRole && a.group_first)
+        // VG (band fill with a strip group table, FillArgs::group_first): a strip group of its own size
+        int vgFirst = 0, vgCount = 0;
+        if constexpr (VG)
         {
-            first = uniform(a.group_first[grp]);
-            count = uniform(a.group_first[grp + 1]) - first;
+            vgFirst = bandRole ? grp * W : uniform(a.group_first[grp]);
+            vgCount = bandRole ? W : uniform(a.group_first[grp + 1]) - vgFirst;
         }
         if (CHAIN && w == W)
         {
-            io_wave(a, strips, nstrips, H.cons, H.drain, rings, first, count, lane);
+            io_wave<VG>(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane, vgFirst, vgCount);
         }
         else if (CHAIN && w > W)
         {
@@ -1749,8 +1754,8 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         }
         else
         {
-            const int idx = first + w;
-            if (w < count && idx < nstrips)
+            const int idx = VG ? vgFirst + w : grp * W + w;
+            if ((!VG || w < vgCount) && idx < nstrips)
             {
                 // the strip kind is compile-time inside process_strip (branch-free body boundaries)
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
@@ -1798,10 +1803,28 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
             if (a.num_bands > 0 && a.A <= 4)
             {
                 // global band fill of a DNA-sized alphabet: the kernel whose bands touch the codes ahead
+                if (a.group_first)
+                {
+                    if (lds > 65536)
+                        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true, true>),
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                    hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
+                    return;
+                }
                 if (lds > 65536)
                     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
+                return;
+            }
+        if constexpr (R == 1 && SK == kArr8)
+            if (a.num_bands > 0 && a.group_first)
+            {
+                // band fill with a strip group table (tail groups of 2 / 1, plan_create)
+                if (lds > 65536)
+                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, false, true>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, false, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
                 return;
             }
         if (lds > 65536)
