@@ -211,9 +211,6 @@ struct Knobs {
     int chain_per_cu = 0;           // SA_CHAIN_PER_CU: 1 / 2 chain workgroups per CU (default: plan_create)
     int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
                                     // capacity (default kBandPersistRows*)
-    int tail_pairs = 1;             // SA_TAIL_PAIRS=0: band fill strip groups all of W (no tail groups of 2)
-    int pair_prio = 0;              // SA_PAIR_PRIO=1: pair-packed fills issue at priority 2 (s_setprio)
-    int64_t tail_lone = -1;         // SA_TAIL_LONE: lone tail strips of a band fill (default: n / 1100)
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
 };
 
@@ -241,9 +238,6 @@ const Knobs &knobs()
         if (const char *e = get("SA_MAX_CUS")) v.max_cus = std::max(0, std::atoi(e));
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
-        if (const char *e = get("SA_TAIL_PAIRS")) v.tail_pairs = std::atoi(e);
-        if (const char *e = get("SA_PAIR_PRIO")) v.pair_prio = std::atoi(e) != 0;
-        if (const char *e = get("SA_TAIL_LONE")) v.tail_lone = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
         return v;
     }();
@@ -311,10 +305,6 @@ struct sa_plan {
     bool band = false;
     std::vector<StripDesc> bands;
     StripDesc *d_bands = nullptr;
-    // band fill: strip groups of 4 and, at the chains' tails, of 2 (FillArgs::group_first; empty:
-    // groups of W)
-    std::vector<int32_t> sgroups;
-    int32_t *d_sgroups = nullptr;
     int num_cu = 0;
     std::vector<PairDesc> pairs;
     std::vector<StripDesc> strips;
@@ -455,7 +445,7 @@ void free_plan(sa_plan *p)
     (void)hipSetDevice(p->device);
     void *bufs[] = {p->d_pairs, p->d_strips, p->d_prof, p->d_table, p->d_codes, p->d_masks, p->d_bnd,
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
-                    p->d_out_pattern, p->d_results, p->d_bands, p->d_sgroups, p->d_tbgroups, p->d_tbpg, p->d_tbl,
+                    p->d_out_pattern, p->d_results, p->d_bands, p->d_tbgroups, p->d_tbpg, p->d_tbl,
                     p->d_gtbl, p->d_gent, p->d_tbflag, p->d_csum, p->d_win, p->d_tbstart, p->d_sent,
                     p->d_sdelta, p->d_send, p->d_pend};
     for (void *b : bufs)
@@ -846,112 +836,30 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
             // nothing); every band publishes its bottom row to granules. The strips keep their planes;
             // a strip at a group start takes its feed from the granules of the band above, the others
             // from the strip above through the group's rings, and a group's last strip publishes nothing.
-            // strip groups: W strips each; with CUs to spare (every group in flight), the latest groups
-            // of the chains split in two, and the very latest into lone strips. A chain's end is its
-            // last strips' n steps, and a strip sharing its CU with three others steps at 44 clk against
-            // 40 beside one other and 35.5 alone (the bands that feed them: 38), so the tail strips
-            // pace closer to the bands. Groups of 4 and 2 start on even strips (band
-            // boundaries); a lone even strip publishes its bottom row to granules for the lone odd strip
-            // below it (one-wave chain hand-off), a lone odd strip publishes nothing.
-            std::vector<int64_t> firsts;
-            std::vector<char> lone;  // per strip: in a group of one
+            granules = 0;
+            for (const PairDesc &d : pl->pairs)
             {
-                const int64_t ns = (int64_t)pl->strips.size();
-                for (int64_t i = 0; i < ns; i += pl->W) firsts.push_back(i);
-                lone.assign(ns, 0);
-                int64_t spare = pl->num_cu - (int64_t)firsts.size() - bandGroups;
-                if (pl->W == 4 && spare > 0 && knobs().tail_pairs != 0 && stripGroups + bandGroups <= pl->num_cu)
+                const uint64_t n = d.text_len;
+                const int B = (d.num_strips + 1) / 2;
+                const int64_t fb = (int64_t)pl->bands.size();
+                for (int b = 0; b + 1 < B; ++b)
                 {
-                    // latest first: by the first strip's row inside its pair
-                    std::vector<int64_t> order;
-                    for (size_t g = 0; g < firsts.size(); ++g)
-                        if (firsts[g] + 2 < ns) order.push_back((int64_t)g);
-                    std::stable_sort(order.begin(), order.end(), [&](int64_t x, int64_t y) {
-                        return pl->strips[firsts[x]].row0 > pl->strips[firsts[y]].row0;
-                    });
-                    // lone strips for the latest ~n/1100 strips of a chain: a strip starts about 53 band
-                    // steps after the one two above it, so over n steps a lone strip (paced by its band)
-                    // gains on a strip in a pair (17.1 vs 16.3 ns per step) what that many strip lags
-                    // cost; groups of 2 for the rest of the spare CUs
-                    int64_t nmax = 0;
-                    for (const PairDesc &d : pl->pairs) nmax = std::max<int64_t>(nmax, (int64_t)d.text_len);
-                    int64_t loneLeft = knobs().tail_lone >= 0 ? knobs().tail_lone : nmax / 1100;
-                    std::vector<int> split(firsts.size(), 0);  // 1: 2 + 2, 2: four lone strips
-                    for (int64_t g : order)
-                    {
-                        const int64_t size = std::min<int64_t>(pl->W, ns - firsts[g]);
-                        if (loneLeft > 0 && size == 4 && spare >= 3)
-                        {
-                            split[g] = 2;
-                            spare -= 3;
-                            loneLeft -= 4;
-                        }
-                        else if (spare >= 1)
-                        {
-                            split[g] = 1;
-                            --spare;
-                        }
-                        else break;
-                    }
-                    std::vector<int64_t> f2;
-                    for (size_t g = 0; g < firsts.size(); ++g)
-                    {
-                        f2.push_back(firsts[g]);
-                        if (split[g] == 1) f2.push_back(firsts[g] + 2);
-                        if (split[g] == 2)
-                        {
-                            for (int q = 1; q < 4; ++q) f2.push_back(firsts[g] + q);
-                            for (int q = 0; q < 4; ++q) lone[firsts[g] + q] = 1;
-                        }
-                    }
-                    firsts.swap(f2);
-                    pl->sgroups.assign(firsts.begin(), firsts.end());
-                    pl->sgroups.push_back((int32_t)ns);
+                    StripDesc bd = pl->strips[d.first_strip + 2 * b];
+                    bd.row0 = 1 + b * 2 * kWave;
+                    bd.flags = (b > 0 ? kHasPrev : 0) | kHasNext;
+                    bd.mask_off = 0;
+                    bd.bnd_in = b > 0 ? pl->bands.back().bnd_out : 0;
+                    bd.bnd_out = granules;
+                    granules += n + 8;
+                    pl->bands.push_back(bd);
                 }
-            }
-            {
-                const int64_t ns = (int64_t)pl->strips.size();
-                std::vector<char> gstart(ns + 1, 0), glast(ns + 1, 0);
-                for (size_t g = 0; g < firsts.size(); ++g)
+                for (int k = 0; k < d.num_strips; ++k)
                 {
-                    gstart[firsts[g]] = 1;
-                    const int64_t end = g + 1 < firsts.size() ? firsts[g + 1] : ns;
-                    glast[end - 1] = 1;
-                }
-                granules = 0;
-                for (const PairDesc &d : pl->pairs)
-                {
-                    const uint64_t n = d.text_len;
-                    const int B = (d.num_strips + 1) / 2;
-                    const int64_t fb = (int64_t)pl->bands.size();
-                    for (int b = 0; b + 1 < B; ++b)
-                    {
-                        StripDesc bd = pl->strips[d.first_strip + 2 * b];
-                        bd.row0 = 1 + b * 2 * kWave;
-                        bd.flags = (b > 0 ? kHasPrev : 0) | kHasNext;
-                        bd.mask_off = 0;
-                        bd.bnd_in = b > 0 ? pl->bands.back().bnd_out : 0;
-                        bd.bnd_out = granules;
-                        granules += n + 8;
-                        pl->bands.push_back(bd);
-                    }
-                    for (int k = 0; k < d.num_strips; ++k)
-                    {
-                        StripDesc &sd = pl->strips[d.first_strip + k];
-                        const int i = d.first_strip + k;
-                        // a lone even strip feeds the strip below through granules of its own
-                        const bool pub = lone[i] && k % 2 == 0 && k + 1 < d.num_strips;
-                        if (k + 1 < d.num_strips && glast[i] && !pub) sd.flags &= ~kHasNext;
-                        sd.bnd_out = 0;
-                        if (pub)
-                        {
-                            sd.bnd_out = granules;
-                            granules += n + 8;
-                        }
-                        sd.bnd_in = (k > 0 && gstart[i]) ? (k % 2 == 0 ? pl->bands[fb + k / 2 - 1].bnd_out
-                                                                       : pl->strips[i - 1].bnd_out)
-                                                         : 0;
-                    }
+                    StripDesc &sd = pl->strips[d.first_strip + k];
+                    const int i = d.first_strip + k;
+                    if (k + 1 < d.num_strips && (i + 1) % pl->W == 0) sd.flags &= ~kHasNext;
+                    sd.bnd_out = 0;
+                    sd.bnd_in = (k > 0 && i % pl->W == 0) ? pl->bands[fb + k / 2 - 1].bnd_out : 0;
                 }
             }
             pl->band = true;
@@ -1016,7 +924,6 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_prof, sizeof(int32_t) * 4},
         {(void **)&pl->d_table, sizeof(int32_t) * A * A},
         {(void **)&pl->d_bands, sizeof(StripDesc) * pl->bands.size()},
-        {(void **)&pl->d_sgroups, sizeof(int32_t) * pl->sgroups.size()},
         {(void **)&pl->d_tbgroups, sizeof(TbGroup) * ntg},
         {(void **)&pl->d_tbpg, ntg ? sizeof(int32_t) * (np + 1) : 0},
         {(void **)&pl->d_ws_text, in ? inN + 16 : 0},
@@ -1082,7 +989,6 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         put(pl->d_prof, prof.data(), sizeof(int32_t) * 4);
         put(pl->d_table, table.data(), sizeof(int32_t) * A * A);
         put(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size());
-        put(pl->d_sgroups, pl->sgroups.data(), sizeof(int32_t) * pl->sgroups.size());
         put(pl->d_tbgroups, pl->tb_groups.data(), sizeof(TbGroup) * ntg);
         if (ntg) put(pl->d_tbpg, pl->tb_pg.data(), sizeof(int32_t) * (np + 1));
         put(pl->d_ws_text, in->text, inN);
@@ -1113,8 +1019,6 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
     if (okc && pl->band)
         okc = hipMemcpyAsync(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size(), hipMemcpyHostToDevice, st) == hipSuccess;
-    if (okc && !pl->sgroups.empty())
-        okc = hipMemcpyAsync(pl->d_sgroups, pl->sgroups.data(), sizeof(int32_t) * pl->sgroups.size(), hipMemcpyHostToDevice, st) == hipSuccess;
     if (okc && ntg)
         okc = hipMemcpyAsync(pl->d_tbgroups, pl->tb_groups.data(), sizeof(TbGroup) * ntg, hipMemcpyHostToDevice, st) == hipSuccess &&
               hipMemcpyAsync(pl->d_tbpg, pl->tb_pg.data(), sizeof(int32_t) * (np + 1), hipMemcpyHostToDevice, st) == hipSuccess;
@@ -1199,8 +1103,6 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.num_band_groups = 0;
         a.band_wgs = 0;
         a.pair_text_len = 0;
-        a.group_first = nullptr;
-        a.pair_prio = knobs().pair_prio;
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;
@@ -1244,11 +1146,6 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             // that they fit): a strip group waits only for bands, which never wait for strips
             a.num_bands = (int32_t)pl->bands.size();
             a.num_band_groups = (a.num_bands + W - 1) / W;
-            if (!pl->sgroups.empty())
-            {
-                a.group_first = pl->d_sgroups;
-                a.num_groups = (int32_t)pl->sgroups.size() - 1;
-            }
             a.band_wgs = a.num_band_groups;
             a.chain_lds = std::max(a.chain_lds, 96 * 1024);
             grid = a.num_band_groups + a.num_groups;

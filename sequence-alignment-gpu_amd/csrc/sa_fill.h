@@ -42,11 +42,6 @@ struct FillArgs {
     int32_t num_band_groups;    // ceil(num_bands / W)
     int32_t band_wgs;
     int32_t pair_text_len;      // pair-packed chains (fill_pair_chain_kernel): the pairs' common text length
-    // band fill: strip group g is strips group_first[g] .. group_first[g + 1] - 1 (groups of 4 and, at
-    // the chain's tail, of 2: fewer waves per CU step faster), or null: groups of W
-    const int32_t *group_first;
-    int32_t pair_prio;          // pair-packed kernels: issue priority (s_setprio) over the waves of
-                                // kernels running beside them (a pipelined batch's traceback)
 };
 
 constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..37: experiment progress stamps)

@@ -1434,7 +1434,6 @@ __global__ __launch_bounds__(kWave * kPairWaves, 2) void fill_pair_kernel(FillAr
     const int w = uniform((int)(threadIdx.x / kWave));
     const int W = (int)(blockDim.x / kWave);
     const int units = a.num_strips / 2;
-    if (a.pair_prio) __builtin_amdgcn_s_setprio(2);
     while (true)
     {
         __syncthreads();
@@ -1460,7 +1459,6 @@ __global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(
     const int u = (int)blockIdx.x;
     const PairDesc pA = a.pairs[2 * u], pB = a.pairs[2 * u + 1];
     const int E = pair_row_entries((int)pA.text_len);
-    if (a.pair_prio) __builtin_amdgcn_s_setprio(2);
     for (int e = threadIdx.x; e < (S - 1) * E; e += blockDim.x) lds_st(prow + e, -1);
     __syncthreads();
     const int sA = uniform(pA.first_strip) + w, sB = uniform(pB.first_strip) + w;
@@ -1476,15 +1474,11 @@ __global__ __launch_bounds__(kWave * kPairChainMax) void fill_pair_chain_kernel(
 // load the fabric the running strips use); the bytes move 64 columns per instruction. Ring entries
 // carry their lap tags both ways (ring_tag), like the compute waves' own hand-offs.
 // (strips: the launch's strips, or its bands in a band workgroup)
-// (VG: the group is strips first .. first + count - 1 of a group table, FillArgs::group_first;
-// otherwise strips grp * W .. grp * W + W - 1: that path's code is kept exactly as it was, since the
-// band loop's pace is sensitive to the code around it)
-template <bool VG = false>
 __device__ __forceinline__ void io_wave(const FillArgs &a, const StripDesc *strips, int nstrips, int *cons, int *drain,
-                                        lds_int *rings, int grp, int W, int lane, int vgFirst = 0, int vgCount = 0)
+                                        lds_int *rings, int grp, int W, int lane)
 {
-    const int first = VG ? vgFirst : grp * W;
-    const int last = min(first + (VG ? vgCount : W), nstrips) - 1;
+    const int first = grp * W;
+    const int last = min(first + W, nstrips) - 1;
     const StripDesc sf = strips[first];
     const StripDesc sl = strips[last];
     const int nIn = (sf.flags & kHasPrev) ? (int)a.pairs[sf.pair].text_len : 0;
@@ -1672,7 +1666,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false, bool VG = false>
+template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -1731,16 +1725,9 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         __syncthreads();
         const int grp = uniform(H.group);
         if (grp >= ngroups) break;
-        // VG (band fill with a strip group table, FillArgs::group_first): a strip group of its own size
-        int vgFirst = 0, vgCount = 0;
-        if constexpr (VG)
-        {
-            vgFirst = bandRole ? grp * W : uniform(a.group_first[grp]);
-            vgCount = bandRole ? W : uniform(a.group_first[grp + 1]) - vgFirst;
-        }
         if (CHAIN && w == W)
         {
-            io_wave<VG>(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane, vgFirst, vgCount);
+            io_wave(a, strips, nstrips, H.cons, H.drain, rings, grp, W, lane);
         }
         else if (CHAIN && w > W)
         {
@@ -1754,8 +1741,8 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
         }
         else
         {
-            const int idx = VG ? vgFirst + w : grp * W + w;
-            if ((!VG || w < vgCount) && idx < nstrips)
+            const int idx = grp * W + w;
+            if (idx < nstrips)
             {
                 // the strip kind is compile-time inside process_strip (branch-free body boundaries)
                 // (CHAIN: some pair has several strips; otherwise every strip is alone and only one
@@ -1803,28 +1790,10 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
             if (a.num_bands > 0 && a.A <= 4)
             {
                 // global band fill of a DNA-sized alphabet: the kernel whose bands touch the codes ahead
-                if (a.group_first)
-                {
-                    if (lds > 65536)
-                        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true, true>),
-                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                    hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
-                    return;
-                }
                 if (lds > 65536)
                     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
-                return;
-            }
-        if constexpr (R == 1 && SK == kArr8)
-            if (a.num_bands > 0 && a.group_first)
-            {
-                // band fill with a strip group table (tail groups of 2 / 1, plan_create)
-                if (lds > 65536)
-                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, false, true>),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, false, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
                 return;
             }
         if (lds > 65536)

@@ -122,18 +122,6 @@ def test_band_fill_default_shapes_vs_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tail", [("1", "0"), ("1", "24"), ("0", "0")])
-def test_band_fill_tail_groups_vs_oracle(tail):
-    """Tail strip groups (plan_create: with CUs to spare, the latest groups of 4 strips split into groups
-    of 2, and the very latest into lone strips, a lone even strip handing its bottom row to the lone odd
-    strip below through granules of its own): groups of 2 only, 24 lone strips plus groups of 2, and
-    groups of 4 only; every cell and the alignments vs the oracle, both modes, in the small cases and
-    the several-pair plans of test_band_fill_vs_oracle."""
-    pairs, lone = tail
-    _run(SMALL, SA_BAND="1", SA_TAIL_PAIRS=pairs, SA_TAIL_LONE=lone)
-
-
-@pytest.mark.gpu
 def test_band_fill_persistent_workers_vs_oracle():
     """SA_MAX_CUS=16 plans a 2048 x 8192 pair (16 band groups + 32 strip groups) on 16 CUs: 5 band and
     11 strip workgroups take their groups from the queues in chain order; every cell of the direction
