@@ -331,6 +331,7 @@ struct sa_plan {
     int32_t *d_tbpg = nullptr, *d_tbl = nullptr, *d_gtbl = nullptr, *d_gent = nullptr, *d_tbflag = nullptr, *d_win = nullptr;
     int32_t *d_tbstart = nullptr, *d_sent = nullptr, *d_sdelta = nullptr, *d_send = nullptr, *d_pend = nullptr;
     int64_t *d_csum = nullptr;  // expansion: per-chunk sums (pairs of more than kChunkRecs records)
+    uint64_t *d_cflag = nullptr;  // expansion: per-chunk epoch flags (ExpandArgs::chunk_flags)
     int64_t max_recs = 1;       // records per pair at most (row walk: pattern rows, column walk: text columns)
     char *d_out_text = nullptr, *d_out_pattern = nullptr;
     sa_result *d_results = nullptr;
@@ -447,7 +448,7 @@ void free_plan(sa_plan *p)
                     p->d_best, p->d_score, p->d_ctrl, p->d_rec, p->d_heads, p->d_out_text,
                     p->d_out_pattern, p->d_results, p->d_bands, p->d_tbgroups, p->d_tbpg, p->d_tbl,
                     p->d_gtbl, p->d_gent, p->d_tbflag, p->d_csum, p->d_win, p->d_tbstart, p->d_sent,
-                    p->d_sdelta, p->d_send, p->d_pend};
+                    p->d_sdelta, p->d_send, p->d_pend, p->d_cflag};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (p->own) (void)hipStreamDestroy(p->own);
@@ -951,6 +952,7 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         {(void **)&pl->d_sdelta, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * nstr : 0},
         {(void **)&pl->d_send, ntg && P->mode == SA_LOCAL ? sizeof(int32_t) * 4 * nstr : 0},
         {(void **)&pl->d_csum, pl->max_recs > kChunkRecs ? sizeof(int64_t) * kMaxChunks * npp : 0},
+        {(void **)&pl->d_cflag, pl->max_recs > kChunkRecs ? sizeof(uint64_t) * kMaxChunks * npp : 0},
     };
     int rc = SA_OK;
     if (ws)
@@ -1017,6 +1019,11 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemcpyAsync(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(pl->d_bnd, 0, bndB, st) == hipSuccess &&
                hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
+    // expansion flags carry the plan's epoch, which starts again at 1 for a plan of its own: a freed
+    // plan's flags at the same address would match (workspace plans draw epochs from their device's
+    // context, which only grow, so their arena needs no clearing)
+    if (okc && pl->d_cflag)
+        okc = hipMemsetAsync(pl->d_cflag, 0, sizeof(uint64_t) * kMaxChunks * npp, st) == hipSuccess;
     if (okc && pl->band)
         okc = hipMemcpyAsync(pl->d_bands, pl->bands.data(), sizeof(StripDesc) * pl->bands.size(), hipMemcpyHostToDevice, st) == hipSuccess;
     if (okc && ntg)
@@ -1297,6 +1304,8 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     x.A = pl->A;
     std::memcpy(x.alphabet, pl->alphabet, 33);
     x.chunk_sums = pl->d_csum;
+    x.chunk_flags = pl->d_cflag;
+    x.epoch = pl->epoch;
     // records per pair: one per row (row walk, R = 1) or per column (column walk)
     launch_expand(x, np, pl->max_recs, st);
     HIP_TRY(hipGetLastError());

@@ -114,6 +114,7 @@ struct TbArgs {
     int32_t A, gap, key_rowbits, local, fast;
     int32_t round, last_round;  // this launch's round of tables (1 ..); the last (a pair still unresolved falls back)
     int32_t strict;             // tests (SA_TB_STRICT): no sequential walk for the pairs the tables leave
+    int32_t ngroups;            // the plan's table groups (tb_walk_kernel: finish blocks follow them)
     uint64_t *dbg;             // debug (SA_TB_TABLE_TIMING): per strip 12 words of tb_table_kernel stamps
 };
 
@@ -141,6 +142,8 @@ struct ExpandArgs {
     int32_t A;
     int32_t chunk_recs;  // records per expansion block (launch_expand sets it)
     int64_t *chunk_sums; // [pair][kMaxChunks] packed op / letter counts per block (pairs of several blocks)
+    uint64_t *chunk_flags; // [pair][kMaxChunks] (epoch << 32) | ~epoch once the block's sums are there
+    uint32_t epoch;      // the plan's fill epoch (tags chunk_flags)
     char alphabet[33];
 };
 
@@ -151,7 +154,7 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st);
 constexpr int kChunkRecs = 2048;    // pairs of at most this many records: one expansion block each
 constexpr int kMinChunkRecs = 256;  // records per block of a longer pair (at least)
 constexpr int kMaxChunks = 256;     // blocks per pair (chunks past a pair's records exit at once)
-// chunk_sums must hold np * kMaxChunks entries when max_records > kChunkRecs
+// chunk_sums and chunk_flags must hold np * kMaxChunks entries when max_records > kChunkRecs
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st);
 
 }  // namespace sa

@@ -668,6 +668,7 @@ __device__ __forceinline__ void walk_rw_pair(const WalkArgs &a, const int p, RwL
     if constexpr (LOCAL)
         for (int e = threadIdx.x; e < a.A * a.A; e += blockDim.x) stab[e] = a.score_tab[e] - a.gap;  // (the table holds S + g)
     __syncthreads();
+    if (threadIdx.x >= 2 * kWave) return;  // (a larger block's other waves: tb_walk_kernel's finish blocks)
     if (threadIdx.x >= kWave)
     {
         // the stager: strips of the pair's chain (R = 1 layout, as the walker computes below)
@@ -1552,10 +1553,27 @@ __global__ __launch_bounds__(1024) void tb_resolve_kernel(TbArgs a)
 // column (each strip's entry), then wave w walks strip sHi - w from its entry with the row walk's
 // staging and unrolled batch and writes its rows' records (record of row i at index i0 - i); local:
 // the strip's entry column and the sum of its H steps (local_check's, see rw_stager_local)
-__global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a)
+// FIN (global): np more blocks after the groups' are tb_finish_kernel<false>'s, block ngroups + p the
+// sequential walk of pair p if the tables left it (one launch less: they run beside the walk blocks,
+// whose pairs the tables resolved, so they touch none of the same pairs)
+template <bool FIN>
+__global__ __launch_bounds__(kTbG * kWave) void tb_walk_kernel(TbArgs a, WalkArgs wa)
 {
     __shared__ int32_t tl[kTbG * kTbK];
     __shared__ int ent[kTbG], wlo[kTbG];
+    if constexpr (FIN)
+    {
+        static_assert(sizeof(RwLds<false>) <= sizeof(tl), "the finish block's LDS lives in the tables' place");
+        if ((int)blockIdx.x >= a.ngroups)
+        {
+            const int p = (int)blockIdx.x - a.ngroups;
+            if (uniform(a.pair_g0[p + 1]) == uniform(a.pair_g0[p])) return;  // (walk_rw_kernel's)
+            if (uniform(a.tb_flag[p]) == 0 || a.strict) return;  // (tb_resolve_kernel wrote the head)
+            walk_rw_pair<false>(wa, p, *reinterpret_cast<RwLds<false> *>(tl));
+            return;
+        }
+    }
+    (void)wa;
     const TbGroup g = a.groups[blockIdx.x];
     const int p = uniform(g.pair);
     if (uniform(a.tb_flag[p]) != 0) return;
@@ -1805,22 +1823,6 @@ __device__ __forceinline__ void expand_records(const TbHead &h, const int32_t *r
     }
 }
 
-// Per-chunk sums of rec_counts (pairs of several chunks)
-__global__ __launch_bounds__(kExpThreads) void expand_sum_kernel(ExpandArgs a)
-{
-    __shared__ int64_t scan[2 * kExpThreads];
-    const int p = blockIdx.y;
-    const int N = a.heads[p].nrec;
-    const int c0 = (int)blockIdx.x * a.chunk_recs;
-    if (N <= a.chunk_recs || c0 >= N) return;  // (uniform per block)
-    const int32_t *rec = a.rec + a.pairs[p].rec_off;
-    const int cend = min(N, c0 + a.chunk_recs);
-    int64_t x = 0, y = 0;
-    for (int q = c0 + (int)threadIdx.x; q < cend; q += kExpThreads) x += rec_counts(rec[q]);
-    block_sum2(x, y, scan);
-    if (threadIdx.x == 0) a.chunk_sums[(int64_t)p * kMaxChunks + blockIdx.x] = x;
-}
-
 __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
 {
     __shared__ int64_t scan[2 * kExpThreads];
@@ -1841,26 +1843,43 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
     char *op = a.out_pattern + pd.out_off;
     const int cend = min(N, c0 + a.chunk_recs);
     const bool whole = c0 == 0 && cend == N;  // (uniform per block)
-    // pass 0 (chunks of a longer pair): totals over the pair and the prefix before this chunk
-    int64_t tot = 0, pre = 0;
-    if (!whole)
-    {
-        const int nch = (N + a.chunk_recs - 1) / a.chunk_recs;
-        for (int c = t; c < nch; c += kExpThreads)
-        {
-            const int64_t x = a.chunk_sums[(int64_t)p * kMaxChunks + c];
-            tot += x;
-            pre += c < (int)blockIdx.x ? x : 0;
-        }
-        block_sum2(tot, pre, scan);
-    }
     // pass 1: this thread's records of the chunk
     const int per = (cend - c0 + kExpThreads - 1) / kExpThreads;
     const int lo = min(cend, c0 + t * per), hi = min(cend, lo + per);
     int64_t mine = 0;
     for (int q = lo; q < hi; ++q) mine += rec_counts(rec[q]);
     int64_t chunkTot;
-    const int64_t ex = block_exclusive_scan(mine, scan, chunkTot) + pre;
+    const int64_t exIn = block_exclusive_scan(mine, scan, chunkTot);
+    // chunks of a longer pair: every block publishes its chunk's sums, then takes the pair's totals and
+    // the prefix before its chunk from all of them. The blocks of one pair wait for each other, so they
+    // must all be resident: a pair has at most kMaxChunks blocks, dispatched together in grid order,
+    // and every pair before it in the grid completes without waiting for later ones. A published sum
+    // carries the fill's epoch in its flag word, (epoch << 32) | ~epoch: no clearing per call (a plan
+    // of its own clears the flags once when created; workspace plans' epochs only grow)
+    int64_t tot = 0, pre = 0;
+    if (!whole)
+    {
+        const uint64_t tag = ((uint64_t)a.epoch << 32) | (uint32_t)~a.epoch;
+        uint64_t *flags = a.chunk_flags + (int64_t)p * kMaxChunks;
+        if (t == 0)
+        {
+            __hip_atomic_store(&a.chunk_sums[(int64_t)p * kMaxChunks + blockIdx.x], chunkTot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&flags[blockIdx.x], tag, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const int nch = (N + a.chunk_recs - 1) / a.chunk_recs;
+        for (int c = t; c < nch; c += kExpThreads)
+        {
+            while (__hip_atomic_load(&flags[c], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != tag)
+                __builtin_amdgcn_s_sleep(2);
+            const int64_t x = __hip_atomic_load(&a.chunk_sums[(int64_t)p * kMaxChunks + c], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+            tot += x;
+            pre += c < (int)blockIdx.x ? x : 0;
+        }
+        block_sum2(tot, pre, scan);
+    }
+    const int64_t ex = exIn + pre;
     if (whole) tot = chunkTot;
     const int64_t totCnt = tot >> 32, totCons = tot & 0xffffffffll;
     const int64_t P0 = ex >> 32, C0 = ex & 0xffffffffll;
@@ -1974,14 +1993,15 @@ void launch_tb(const TbArgs &args, const WalkArgs &w, int nstrips, int ngroups, 
         hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
         hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
     }
-    hipLaunchKernelGGL(tb_walk_kernel, dim3(ngroups), dim3(kTbG * kWave), 0, st, a);
+    a.ngroups = ngroups;
     if (a.local)
     {
+        hipLaunchKernelGGL(tb_walk_kernel<false>, dim3(ngroups), dim3(kTbG * kWave), 0, st, a, w);
         hipLaunchKernelGGL(tb_check_kernel, dim3(nstrips), dim3(kWave), 0, st, a);
         hipLaunchKernelGGL(tb_finish_kernel<true>, dim3(np), dim3(2 * kWave), 0, st, a, w);
     }
     else
-        hipLaunchKernelGGL(tb_finish_kernel<false>, dim3(np), dim3(2 * kWave), 0, st, a, w);
+        hipLaunchKernelGGL(tb_walk_kernel<true>, dim3(ngroups + np), dim3(kTbG * kWave), 0, st, a, w);  // (+ finish)
 }
 
 void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t st)
@@ -1991,7 +2011,6 @@ void launch_expand(const ExpandArgs &a, int np, int64_t max_records, hipStream_t
     const int64_t per = recs <= kChunkRecs ? kChunkRecs : std::max<int64_t>(kMinChunkRecs, (recs + kMaxChunks - 1) / kMaxChunks);
     x.chunk_recs = (int)per;
     const int chunks = (int)((recs + per - 1) / per);
-    if (chunks > 1) hipLaunchKernelGGL(expand_sum_kernel, dim3(chunks, np), dim3(kExpThreads), 0, st, x);
     hipLaunchKernelGGL(expand_kernel, dim3(chunks, np), dim3(kExpThreads), 0, st, x);
 }
 
