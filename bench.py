@@ -366,8 +366,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SA_BENCH_ONE_DEVICE=1 (tests on a one-GPU box): every rank on device 0 and the gloo backend (RCCL
+    # needs a device per rank), so the N-rank step, its pipelining and its result gather run for real
+    one_device = world > 1 and os.environ.get("SA_BENCH_ONE_DEVICE") == "1"
+    if one_device:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if one_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     from sa_amd import distributed, synthetic
     from sa_amd.batch import DeviceBatch
@@ -515,7 +523,7 @@ def main():
     tmax = elapsed
     scores = [int(x) for x in res["score"]]
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if one_device else "cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         tmax = float(tt.item())
         if args.workload == "batch":

@@ -58,6 +58,8 @@ def gather_device(buf, num_pairs: int, world: int, rank: int):
     import torch
     import torch.distributed as dist
 
+    if buf.is_cuda and dist.get_backend() == "gloo":
+        buf = buf.cpu()  # (gloo gathers host tensors: the tests' one-GPU, several-rank runs)
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
     dist.gather(buf, parts, dst=0)
     if rank != 0:

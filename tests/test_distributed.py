@@ -217,3 +217,29 @@ def test_bench_refuses_world_size_mismatch():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dry-run"], env=env,
                          capture_output=True, text=True, timeout=120)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload,pair0", [("batch", 1408), ("dna8k", None)])
+def test_bench_two_ranks_on_one_gpu(workload, pair0):
+    """The N-rank bench path for real, on a one-GPU box: `bench.py --gpus 2` launches two ranks, both
+    on device 0 with the gloo backend (SA_BENCH_ONE_DEVICE; RCCL needs a device per rank). The batch
+    deals pairs i mod 2, pipelines each rank's steps two deep and gathers every step's results to rank
+    0 on the traceback stream; the line reports both ranks' pairs (4096), and pair 0's score is the
+    reference's (tests/golden/batch.json.gz). RCCL across devices is what this cannot cover."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["SA_BENCH_ONE_DEVICE"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", workload,
+                          "--steps", "3", "--warmup", "1", "--no-cpu-baseline"], env=env, capture_output=True, text=True,
+                         timeout=170)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["value"] > 0, d
+    if workload == "batch":
+        assert d["sample_result"]["pairs_per_gpu"] == 2048 and d["sample_result"]["pair0_score"] == pair0, d
+        assert d["config"]["step_overlap"].startswith("two-deep"), d
