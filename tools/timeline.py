@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--pairs", type=int, default=1, help="independent copies of the pair (contention test)")
     ap.add_argument("--score", default="blast", help="blast (+5/-4) or MATCH,MISMATCH (e.g. 1,-3)")
     ap.add_argument("--protein", action="store_true", help="BLOSUM50, letters 0..21 (the harness's dummy requests)")
+    ap.add_argument("--letters", type=int, default=0, help="--protein: draw the sequences from letters 0..K-1 only")
     args = ap.parse_args()
     if args.waves:
         os.environ["SA_WAVES_PER_GROUP"] = str(args.waves)
@@ -104,6 +105,8 @@ def main():
         S = np.array(json.load(open(os.path.join(ROOT, "tests", "golden", "matrices.json")))["blosum50"],
                      np.int32).reshape(23, 23)
         A = 22
+        if args.letters > 0:
+            A = args.letters
     t = synthetic.random_sequence(6, args.n, A)
     p = synthetic.random_sequence(7, args.m, A)
     b = DeviceBatch(args.mode, S, 5, [t] * args.pairs, [p] * args.pairs, rows_per_lane=args.R)
