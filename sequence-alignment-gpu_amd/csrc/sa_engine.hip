@@ -212,7 +212,6 @@ struct Knobs {
     int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
                                     // capacity (default kBandPersistRows*)
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
-    int unal = -1;                  // SA_UNAL: 1 / 0 force the unaligned text-profile reads on / off (default: A > 4)
 };
 
 const Knobs &knobs()
@@ -240,7 +239,6 @@ const Knobs &knobs()
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
-        if (const char *e = get("SA_UNAL")) v.unal = std::atoi(e) != 0 ? 1 : 0;
         return v;
     }();
     return k;
@@ -1112,8 +1110,6 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
         a.num_band_groups = 0;
         a.band_wgs = 0;
         a.pair_text_len = 0;
-        // text profiles of more than 4 letters: unaligned copy-0 reads (sa_fill.hip UNAL); SA_UNAL=0/1 forces
-        a.unal_codes = pl->sk == kArr8 && (knobs().unal >= 0 ? knobs().unal == 1 : pl->A > 4);
         // SA_TIMELINE=<file>: debug dump of per-strip timestamps (s_memrealtime, 100 MHz)
         const char *tlPath = knobs().timeline;
         a.timeline = nullptr;

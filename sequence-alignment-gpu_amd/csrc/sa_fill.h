@@ -42,7 +42,6 @@ struct FillArgs {
     int32_t num_band_groups;    // ceil(num_bands / W)
     int32_t band_wgs;
     int32_t pair_text_len;      // pair-packed chains (fill_pair_chain_kernel): the pairs' common text length
-    int32_t unal_codes;         // R = 1 kArr8 chains: read copy 0 of the text profiles unaligned (UNAL)
 };
 
 constexpr int kTimelineWords = 48;  // SA_TIMELINE record per strip, then per band (words 6..37: experiment progress stamps)

@@ -369,12 +369,7 @@ __device__ __forceinline__ void band_steps_asm(BandRegs &r);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
 // kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
-// UNAL (text profiles of more than a few letters, FillArgs::unal_codes): every lane reads copy 0 of
-// its row letter's profile at its own byte offset (an unaligned 16-byte buffer load) instead of copy
-// k % 4 at a dword offset, so the lanes of a wave that share a letter share its cache lines: with 20
-// letters the four copies put a wave's 64 loads on up to 64 distinct lines, and the band step was
-// 52.9 clk against 43.0 with the same kernel on 8 letters or fewer (profiles/r06/protein_letters_v1.log)
-template <int R, bool LOCAL, int SK, bool HP, bool HN, bool UNAL = false>
+template <int R, bool LOCAL, int SK, bool HP, bool HN>
 __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
@@ -413,8 +408,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     uint32_t coff;
     if constexpr (SK == kArr8)
         // byte copy r = k % 4 of letter a: byte kPad + x holds S[a][t[x - r]]; read from x = s0 - (k & ~3)
-        coff = UNAL ? (uint32_t)((uint64_t)prof[0] * 4 * pd.code_len + kPad - lane)
-                    : (uint32_t)(((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+        coff = (uint32_t)(((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
     else if constexpr (SK == kArr)
         coff = (uint32_t)(((uint64_t)prof[0] * pd.code_len + kPad - lane) * 4);
     else
@@ -926,7 +920,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 // the same inputs). Bands exist for every band of a pair but its last (whose bottom row feeds
 // nothing) and need no final state; the local recurrence saturates H = X - g at 0 with one clamped
 // subtract (g >= 0, X >= 0), so local is banded as well.
-template <bool LOCAL, bool HP, bool HN, bool TOUCH, bool UNAL = false>
+template <bool LOCAL, bool HP, bool HN, bool TOUCH>
 __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = 16;
@@ -950,8 +944,7 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         const int i = sd.row0 + 2 * lane + rho;
         int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
         c = min(max(c, 0), a.A - 1);
-        coff[rho] = UNAL ? (uint32_t)((uint64_t)c * 4 * pd.code_len + kPad - lane)
-                         : (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+        coff[rho] = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
     });
     const __amdgpu_buffer_rsrc_t crsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
@@ -1673,7 +1666,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false, bool UNAL = false>
+template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -1763,17 +1756,17 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
                         // -0.8 % fill for round 3's score waves, profiles/r03/dual_dev/prio_timeline.log)
                         __builtin_amdgcn_s_setprio(2);
                         // (every band publishes its bottom row: kHasNext)
-                        if (f & kHasPrev) process_band<LOCAL, true, true, TOUCH, UNAL>(a, L, rings, idx, w, lane);
-                        else process_band<LOCAL, false, true, TOUCH, UNAL>(a, L, rings, idx, w, lane);
+                        if (f & kHasPrev) process_band<LOCAL, true, true, TOUCH>(a, L, rings, idx, w, lane);
+                        else process_band<LOCAL, false, true, TOUCH>(a, L, rings, idx, w, lane);
                         __builtin_amdgcn_s_setprio(0);
                         continue;
                     }
                 if constexpr (CHAIN)
                 {
-                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true, UNAL>(a, L, rings, idx, w, lane);
-                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false, UNAL>(a, L, rings, idx, w, lane);
-                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true, UNAL>(a, L, rings, idx, w, lane);
-                    else process_strip<R, LOCAL, SK, false, false, UNAL>(a, L, rings, idx, w, lane);
+                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
+                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
+                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, L, rings, idx, w, lane);
+                    else process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
                 }
                 else
                 {
@@ -1801,17 +1794,6 @@ void launch_fill_t(const FillArgs &a, int grid, int W, bool chain, hipStream_t s
                     (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, true>),
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
                 hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, true>), dim3(grid), dim3(kWave * (W + 1 + kDrainWaves)), lds, st, a);
-                return;
-            }
-        if constexpr (R == 1 && SK == kArr8)
-            if (a.unal_codes)
-            {
-                // text profiles read unaligned (process_strip, UNAL): alphabets of more than a few letters
-                if (lds > 65536)
-                    (void)hipFuncSetAttribute(reinterpret_cast<const void *>(&fill_kernel<R, LOCAL, SK, true, false, true>),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                hipLaunchKernelGGL((fill_kernel<R, LOCAL, SK, true, false, true>), dim3(grid),
-                                   dim3(kWave * (W + 1 + (a.num_bands > 0 ? kDrainWaves : 0))), lds, st, a);
                 return;
             }
         if (lds > 65536)
