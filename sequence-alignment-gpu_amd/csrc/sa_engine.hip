@@ -212,6 +212,7 @@ struct Knobs {
     int64_t band_rows = 0;          // SA_BAND_ROWS: band fill up to this many rows past resident
                                     // capacity (default kBandPersistRows*)
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
+    int tb_cap = 0;                 // SA_TB_CAP: column-walk waves at most (0: one per pair)
 };
 
 const Knobs &knobs()
@@ -239,6 +240,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_CHAIN_PER_CU")) v.chain_per_cu = std::min(2, std::max(0, std::atoi(e)));
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
+        if (const char *e = get("SA_TB_CAP")) v.tb_cap = std::max(0, std::atoi(e));
         return v;
     }();
     return k;
@@ -1223,6 +1225,7 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
     w.score_tab = pl->d_table;
     w.A = pl->A;
     w.tb_pg = nullptr;
+    w.cap = kn.tb_cap;
     if (!pl->tb_groups.empty())
     {
         // table traceback; its last kernel walks the pairs the tables leave, so the sequential walk

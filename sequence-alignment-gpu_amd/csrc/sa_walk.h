@@ -50,6 +50,7 @@ struct WalkArgs {
     // table traceback (R = 1, see TbGroup): walk_rw_kernel walks only the pairs without groups
     // (tb_finish_kernel walks those the tables leave)
     const int32_t *tb_pg;          // TbArgs::pair_g0, or null: every pair
+    int32_t cap;                   // column walk: at most this many waves, each walking pairs in turn (0: one per pair)
 };
 
 // TABLE TRACEBACK (R = 1 plans; sa_walk.hip tb_*_kernel). The sequential walk of a long pair costs

@@ -973,10 +973,20 @@ __global__ __launch_bounds__(2 * kWave) void walk_rw_kernel(WalkArgs a)
 
 // Column walk (R >= 2): one wave per pair
 template <int R, bool LOCAL>
-__global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a)
+__device__ __forceinline__ void walk_cw_pair(const WalkArgs &a, const int p, uint32_t *cwbuf);
+
+// (np pairs; a grid smaller than np walks them in turn: WalkArgs::cap, the pipelined batch's
+// traceback beside the next fill)
+template <int R, bool LOCAL>
+__global__ __launch_bounds__(64) void walk_cw_kernel(WalkArgs a, int np)
 {
     __shared__ uint32_t cwbuf[R == 32 ? 2 * kCwDw : 1];
-    const int p = blockIdx.x;
+    for (int p = blockIdx.x; p < np; p += gridDim.x) walk_cw_pair<R, LOCAL>(a, p, cwbuf);
+}
+
+template <int R, bool LOCAL>
+__device__ __forceinline__ void walk_cw_pair(const WalkArgs &a, const int p, uint32_t *cwbuf)
+{
     const int lane = threadIdx.x;
     PairDesc pd = a.pairs[p];
     const int n = uniform((int)pd.text_len), m = uniform((int)pd.pattern_len);
@@ -1965,14 +1975,15 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
 template <bool LOCAL>
 void launch_walk_m(int R, const WalkArgs &a, int np, hipStream_t st)
 {
+    const int grid = a.cap > 0 ? std::min(np, a.cap) : np;
     switch (R)
     {
     case 1: hipLaunchKernelGGL(walk_rw_kernel<LOCAL>, dim3(np), dim3(2 * kWave), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((walk_cw_kernel<2, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((walk_cw_kernel<4, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
-    case 8: hipLaunchKernelGGL((walk_cw_kernel<8, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
-    case 16: hipLaunchKernelGGL((walk_cw_kernel<16, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
-    default: hipLaunchKernelGGL((walk_cw_kernel<32, LOCAL>), dim3(np), dim3(kWave), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((walk_cw_kernel<2, LOCAL>), dim3(grid), dim3(kWave), 0, st, a, np); break;
+    case 4: hipLaunchKernelGGL((walk_cw_kernel<4, LOCAL>), dim3(grid), dim3(kWave), 0, st, a, np); break;
+    case 8: hipLaunchKernelGGL((walk_cw_kernel<8, LOCAL>), dim3(grid), dim3(kWave), 0, st, a, np); break;
+    case 16: hipLaunchKernelGGL((walk_cw_kernel<16, LOCAL>), dim3(grid), dim3(kWave), 0, st, a, np); break;
+    default: hipLaunchKernelGGL((walk_cw_kernel<32, LOCAL>), dim3(grid), dim3(kWave), 0, st, a, np); break;
     }
 }
 
