@@ -68,14 +68,21 @@ __host__ __device__ constexpr int pair_row_entries(int n) { return (n + kPairFee
 //           add itself (SDWA src1_sel:BYTE_q, sign-extended).
 //   kPair   pair-packed strips (fill_pair_kernel; chains: fill_pair_chain_kernel): per column the
 //           two pairs' column profiles.
+//   kArr8A  (a launch selector, not a plan's kind) kArr8 chains of alphabets larger than 4: every
+//           lane reads copy 0 of its letters only, dword aligned, and shifts the bytes into place
+//           with v_alignbyte (fill_r1a.hip, launch_fill_align). A wave's 64 lanes then touch one
+//           array per letter instead of one per letter and copy: the CU's L1 holds the working set.
 // The zero padding of the profiles keeps the ramp cells left of column 1 at the boundary value.
-enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3, kPair = 4 };
+enum ScoreKind { kProf = 0, kTable = 1, kArr = 2, kArr8 = 3, kPair = 4, kArr8A = 5 };
 template <int SK>
 constexpr bool kIsArr = SK == kArr || SK == kArr8;
 
 // Fill launch for strip height R (instantiated in fill_r<R>.hip).
 template <int R>
 void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool chain, hipStream_t st);
+// R = 1 kArr8 chains read through copy 0 (kArr8A; fill_r1a.hip, a code object of its own so that the
+// DNA kernels' code and placement stay as they are)
+void launch_fill_align(const FillArgs &a, bool local, int grid, int W, hipStream_t st);
 #ifndef SA_FILL_R
 extern template void launch_fill_r<1>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
 extern template void launch_fill_r<2>(const FillArgs &, bool, int, int, int, bool, hipStream_t);

@@ -369,7 +369,7 @@ __device__ __forceinline__ void band_steps_asm(BandRegs &r);
 // compile-time, so a body boundary carries no per-body decisions. Bodies run in pairs (the text
 // codes double-buffer across the two bodies of a pair) in three phases: ramp pairs (kStart, only
 // kProf / kTable), steady pairs, and tail pairs (kGeneric, only where the final state is read).
-template <int R, bool LOCAL, int SK, bool HP, bool HN>
+template <int R, bool LOCAL, int SK, bool HP, bool HN, bool ALIGN = false>
 __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = Cfg<R>::U;
@@ -406,7 +406,13 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     // SGPR base and one 32-bit add, without 64-bit VALU address arithmetic.
     const char *cbase = reinterpret_cast<const char *>(a.codes + pd.code_off);
     uint32_t coff;
-    if constexpr (SK == kArr8)
+    static_assert(!ALIGN || (R == 1 && SK == kArr8), "kArr8A is the R = 1 kArr8 layout read through copy 0");
+    if constexpr (ALIGN)
+        // kArr8A: copy 0 of letter a (byte kPad + x holds S[a][t[x]]); the body's 16 bytes start at
+        // x = s0 - k, i.e. byte ash = (kPad - k) & 3 of the dword at x4 = s0 + ((kPad - k) & ~3). The
+        // loads fetch the four dwords after x4 and the body takes x4's dword from the body before
+        coff = (uint32_t)((uint64_t)prof[0] * 4 * pd.code_len + ((kPad - lane) & ~3) + 4);
+    else if constexpr (SK == kArr8)
         // byte copy r = k % 4 of letter a: byte kPad + x holds S[a][t[x - r]]; read from x = s0 - (k & ~3)
         coff = (uint32_t)(((uint64_t)prof[0] * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
     else if constexpr (SK == kArr)
@@ -459,6 +465,10 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
     // load and a chunk's store need no VALU address arithmetic and no 64-bit adds
     constexpr bool kBuf = R == 1;
     const __amdgpu_buffer_rsrc_t crsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(cbase), 0, 0x7fffffff, kBufRsrcWord3);
+    // kArr8A: the byte shift of the lane's window and the dword before the next body's four
+    const uint32_t ash = (uint32_t)((kPad - lane) & 3);
+    int wprev = 0;
+    if constexpr (ALIGN) wprev = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff - 4, 0, 0);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(mbase, 0, 0x7ffffff0, kBufRsrcWord3);
     auto load_codes = [&](int s0, int (&dst)[NT]) __attribute__((always_inline)) {
         typedef int i32x4u __attribute__((ext_vector_type(4), aligned(4)));
@@ -681,6 +691,17 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
         }
 #endif
         load_codes(s0 + kAhead * U, Tn);
+        if constexpr (ALIGN)
+        {
+            // the body's 16 score bytes into place (in the buffer itself: its raw words are not read
+            // again), the last raw dword kept for the next body
+            const int w4 = T[3];
+            T[3] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[3], (uint32_t)T[2], ash);
+            T[2] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[2], (uint32_t)T[1], ash);
+            T[1] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[1], (uint32_t)T[0], ash);
+            T[0] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[0], (uint32_t)wprev, ash);
+            wprev = w4;
+        }
         if constexpr (kAsm && KIND == kSteady)
         {
             static_assert(U == 16 && NT == 4, "sa_fill_steps.inc is generated for these");
@@ -920,7 +941,7 @@ __device__ __forceinline__ void process_strip(const FillArgs &a, const StripLds 
 // the same inputs). Bands exist for every band of a pair but its last (whose bottom row feeds
 // nothing) and need no final state; the local recurrence saturates H = X - g at 0 with one clamped
 // subtract (g >= 0, X >= 0), so local is banded as well.
-template <bool LOCAL, bool HP, bool HN, bool TOUCH>
+template <bool LOCAL, bool HP, bool HN, bool TOUCH, bool ALIGN = false>
 __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &L, lds_int *rings, int idx, int w, int lane)
 {
     constexpr int U = 16;
@@ -944,7 +965,11 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         const int i = sd.row0 + 2 * lane + rho;
         int c = i <= m ? (int)a.pattern[pd.pattern_off + i - 1] : 0;
         c = min(max(c, 0), a.A - 1);
-        coff[rho] = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
+        if constexpr (ALIGN)
+            // kArr8A: copy 0, dword aligned, shifted in registers (process_strip)
+            coff[rho] = (uint32_t)((uint64_t)c * 4 * pd.code_len + ((kPad - lane) & ~3) + 4);
+        else
+            coff[rho] = (uint32_t)(((uint64_t)c * 4 + (lane & 3)) * pd.code_len + kPad - (lane & ~3));
     });
     const __amdgpu_buffer_rsrc_t crsrc =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(a.codes + pd.code_off), 0, 0x7fffffff, kBufRsrcWord3);
@@ -1071,6 +1096,13 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
     asm volatile("v_mov_b32 %0, 0x80000000" : "=v"(msbv));
     const uint64_t tStart = a.timeline ? now_ticks() : 0;
     int TA0[4], TA1[4], TB0[4], TB1[4], TC0[4], TC1[4], TD0[4], TD1[4];
+    const uint32_t ash = (uint32_t)((kPad - lane) & 3);
+    int wprev0 = 0, wprev1 = 0;  // kArr8A: the dword before the next body's four, per row
+    if constexpr (ALIGN)
+    {
+        wprev0 = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff[0] - 4, 0, 0);
+        wprev1 = __builtin_amdgcn_raw_buffer_load_b32(crsrc, coff[1] - 4, 0, 0);
+    }
     load_codes(0, TA0, TA1);
     // TA's two loads before TB's, as in the steady quads: otherwise the loop's first body waits for
     // one of the previous body's loads in every quad (vmcnt(3) instead of (4))
@@ -1095,6 +1127,19 @@ __device__ __forceinline__ void process_band(const FillArgs &a, const StripLds &
         constexpr bool FULL = decltype(full)::value;
         const int s1 = s0 + U;
         load_codes(s0 + 2 * U, Tn0, Tn1);
+        if constexpr (ALIGN)
+        {
+            auto shift = [&](int(&T)[4], int &wp) __attribute__((always_inline)) {
+                const int w4 = T[3];
+                T[3] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[3], (uint32_t)T[2], ash);
+                T[2] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[2], (uint32_t)T[1], ash);
+                T[1] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[1], (uint32_t)T[0], ash);
+                T[0] = (int)__builtin_amdgcn_alignbyte((uint32_t)T[0], (uint32_t)wp, ash);
+                wp = w4;
+            };
+            shift(T0, wprev0);
+            shift(T1, wprev1);
+        }
         BandRegs r;
         r.Q = Q;
         r.diag = diag;
@@ -1666,7 +1711,7 @@ __device__ __forceinline__ void drain_wave(const FillArgs &a, int *drain, lds_in
 // One workgroup = W compute waves + 1 I/O wave; it takes groups of W consecutive strips from the
 // dynamic queue until the queue is empty. The queue order is the strip order, so a strip's
 // predecessor has always been handed out before it: progress is guaranteed whatever the residency.
-template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false>
+template <int R, bool LOCAL, int SK, bool CHAIN, bool TOUCH = false, bool ALIGN = false>
 __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_kernel(FillArgs a)
 {
     extern __shared__ int lds_dyn[];
@@ -1756,17 +1801,17 @@ __global__ __launch_bounds__(kWave * (kMaxWaves + 1 + kDrainWaves)) void fill_ke
                         // -0.8 % fill for round 3's score waves, profiles/r03/dual_dev/prio_timeline.log)
                         __builtin_amdgcn_s_setprio(2);
                         // (every band publishes its bottom row: kHasNext)
-                        if (f & kHasPrev) process_band<LOCAL, true, true, TOUCH>(a, L, rings, idx, w, lane);
-                        else process_band<LOCAL, false, true, TOUCH>(a, L, rings, idx, w, lane);
+                        if (f & kHasPrev) process_band<LOCAL, true, true, TOUCH, ALIGN>(a, L, rings, idx, w, lane);
+                        else process_band<LOCAL, false, true, TOUCH, ALIGN>(a, L, rings, idx, w, lane);
                         __builtin_amdgcn_s_setprio(0);
                         continue;
                     }
                 if constexpr (CHAIN)
                 {
-                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true>(a, L, rings, idx, w, lane);
-                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false>(a, L, rings, idx, w, lane);
-                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true>(a, L, rings, idx, w, lane);
-                    else process_strip<R, LOCAL, SK, false, false>(a, L, rings, idx, w, lane);
+                    if (f == (kHasPrev | kHasNext)) process_strip<R, LOCAL, SK, true, true, ALIGN>(a, L, rings, idx, w, lane);
+                    else if (f == kHasPrev) process_strip<R, LOCAL, SK, true, false, ALIGN>(a, L, rings, idx, w, lane);
+                    else if (f == kHasNext) process_strip<R, LOCAL, SK, false, true, ALIGN>(a, L, rings, idx, w, lane);
+                    else process_strip<R, LOCAL, SK, false, false, ALIGN>(a, L, rings, idx, w, lane);
                 }
                 else
                 {
@@ -1811,7 +1856,8 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
 {
     if constexpr (R == 1)
     {
-        if (sk == kArr8)
+        if (sk == kArr8A && chain) launch_fill_align(a, local, grid, W, st);
+        else if (sk == kArr8 || sk == kArr8A)
         {
             if (local) launch_fill_t<1, true, kArr8>(a, grid, W, chain, st);
             else launch_fill_t<1, false, kArr8>(a, grid, W, chain, st);
@@ -1850,6 +1896,22 @@ void launch_fill_r(const FillArgs &a, bool local, int sk, int grid, int W, bool 
     }
 }
 
+#ifdef SA_FILL_ALIGN
+// fill_r1a.hip: the kArr8A chain kernels (bands and strips read copy 0 of the text profiles)
+void launch_fill_align(const FillArgs &a, bool local, int grid, int W, hipStream_t st)
+{
+    const size_t lds = std::max(group_lds_bytes(W), (size_t)a.chain_lds);
+    const dim3 block(kWave * (W + 1 + (a.num_bands > 0 ? kDrainWaves : 0)));
+    auto go = [&](auto kern) {
+        if (lds > 65536)
+            (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(grid), block, lds, st, a);
+    };
+    if (local) go(&fill_kernel<1, true, kArr8, true, false, true>);
+    else go(&fill_kernel<1, false, kArr8, true, false, true>);
+}
+#else
 template void launch_fill_r<SA_FILL_R>(const FillArgs &, bool, int, int, int, bool, hipStream_t);
+#endif
 
 }  // namespace sa

@@ -17,7 +17,7 @@ fi
 flags="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$root/include -I$src -DSA_EXPERIMENT=1 $*"
 # EXP_ONLY="fill_r1 ..." recompiles only those units and takes the others from the product build
 pids=()
-for f in sa_engine sa_walk sa_batch fill_r1 fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
+for f in sa_engine sa_walk sa_batch fill_r1 fill_r1a fill_r2 fill_r4 fill_r8 fill_r16 fill_r32; do
   if [ -n "$EXP_ONLY" ] && [[ " $EXP_ONLY " != *" $f "* ]]; then
     cp $root/sequence-alignment-gpu_amd/build/$f.o $out/$f.o
   else
