@@ -213,9 +213,9 @@ struct Knobs {
                                     // capacity (default kBandPersistRows*)
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
     int tb_cap = 0;                 // SA_TB_CAP: column-walk waves at most (0: one per pair)
-    bool align = true;              // SA_ALIGN=0: chains of alphabets larger than 4 read the four
+    int align = 1;                  // SA_ALIGN=0: chains of alphabets larger than 4 read the four
                                     // byte copies of their text profiles (kArr8) instead of copy 0
-                                    // shifted in registers (kArr8A)
+                                    // shifted in registers (kArr8A); 2: every alphabet (experiments)
 };
 
 const Knobs &knobs()
@@ -244,7 +244,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
         if (const char *e = get("SA_TB_CAP")) v.tb_cap = std::max(0, std::atoi(e));
-        if (const char *e = get("SA_ALIGN")) v.align = std::atoi(e) != 0;
+        if (const char *e = get("SA_ALIGN")) v.align = std::min(2, std::max(0, std::atoi(e)));
         return v;
     }();
     return k;
@@ -1173,7 +1173,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             }
         }
         // chains of protein-sized alphabets read copy 0 of their text profiles (kArr8A, sa_fill.h)
-        const int sk = pl->sk == kArr8 && pl->chain && pl->A > 4 && knobs().align ? kArr8A : pl->sk;
+        const int sk = pl->sk == kArr8 && pl->chain && knobs().align > (pl->A > 4 ? 0 : 1) ? kArr8A : pl->sk;
         launch_fill(pl->R, a, pl->mode == SA_LOCAL, sk, grid, pl->sk == kPair && pl->chain ? pl->pairs[0].num_strips : W,
                     pl->chain, st);
         HIP_TRY(hipGetLastError());

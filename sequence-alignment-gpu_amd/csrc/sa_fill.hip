@@ -1907,6 +1907,10 @@ void launch_fill_align(const FillArgs &a, bool local, int grid, int W, hipStream
             (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(grid), block, lds, st, a);
     };
+#if defined(SA_EXPERIMENT) && defined(SA_EXP_ALIGN_TOUCH)
+    // experiment: global bands touch the code lines ahead (the DNA kernel's TOUCH)
+    if (!local) return go(&fill_kernel<1, false, kArr8, true, true, true>);
+#endif
     if (local) go(&fill_kernel<1, true, kArr8, true, false, true>);
     else go(&fill_kernel<1, false, kArr8, true, false, true>);
 }
