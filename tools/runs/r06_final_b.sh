@@ -9,5 +9,5 @@ done
 for n in 2 4 8; do
   timeout -k 10 300 python bench.py --workload batch --shard-of $n --steps 20 --no-cpu-baseline > gpurun_out/r6f_shard_of_$n.json 2> gpurun_out/r6f_shard_of_$n.err || { tail gpurun_out/r6f_shard_of_$n.err; exit 1; }
 done
-timeout -k 10 900 bash tools/harness.sh r6f > gpurun_out/r6f_harness.log 2>&1 || { tail -20 gpurun_out/r6f_harness.log; exit 1; }
+timeout -k 10 900 bash tools/harness.sh r6f > gpurun_out/r6f_harness_run.log 2>&1 || { tail -20 gpurun_out/r6f_harness_run.log; exit 1; }
 echo final_b done
