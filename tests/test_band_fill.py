@@ -6,7 +6,8 @@ DIRECTION matrix (alignSequenceCPU.cpp:116-201 local, :203-284 global) and the f
 (:10-114), for both modes and gaps 5 / 0 (and -2, global only: local kArr8 needs g >= 0, the plan
 falls back to the one-wave fill there); at the default shapes (>= 16384 columns, several band and
 strip groups); more groups than CUs (SA_MAX_CUS: persistent band and strip workers); a 23-letter
-BLOSUM50 pair in both modes (the global band kernel without the code touch); with several chained pairs per plan (band groups spanning pairs); and a local then a
+BLOSUM50 pair in both modes (the global band kernel without the code touch); protein chains reading copy 0
+of their text profiles (kArr8A) with SA_ALIGN=1 / 0 / 2; with several chained pairs per plan (band groups spanning pairs); and a local then a
 global 32768^2 call in one fresh process, against the reference's recorded outputs (large.json)."""
 from __future__ import annotations
 
@@ -101,6 +102,30 @@ for name in ("cfg3_dna_local_32768_uniform", "headline_dna_global_32768_uniform"
         bad.append(name)
 print("BAND_OK" if not bad else "BAND_BAD %r" % (bad,))
 '''
+
+
+# protein chains read copy 0 of their text profiles and shift the bytes in registers (kArr8A,
+# sa_fill.h; SA_ALIGN=0: the four byte copies; 2: DNA as well): text lengths of every residue mod 4
+# and mod 16 (the lane windows' byte shifts and the last body's padding), band and one-wave chains,
+# both modes, cell by cell
+ALIGN = HEAD + r'''
+B50 = np.array(json.load(open(sys.argv[1] + "/tests/golden/matrices.json"))["blosum50"], np.int32).reshape(23, 23)
+B62 = np.array(json.load(open(sys.argv[1] + "/tests/golden/matrices.json"))["blosum62"], np.int32).reshape(23, 23)
+cases = [(3001, 1100, 5), (2998, 700, 0), (1283, 1500, 3), (4099, 257, 5), (515, 640, 5)]
+for k, (n, m, gap) in enumerate(cases):
+    for mode in (0, 1):
+        check(mode, n, m, gap, 1200 + 10 * k, k % 2 == 1, S=B50 if k % 2 == 0 else B62)
+check(0, 2500, 900, 5, 1300, True)  # DNA (copy-0 reads only with SA_ALIGN=2)
+check(1, 2047, 1300, 5, 1310, False)
+print("BAND_OK" if not bad else "BAND_BAD %r" % (bad,))
+'''
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("align", ["1", "0", "2"])
+@pytest.mark.parametrize("band", ["1", "0"])
+def test_copy0_profile_reads_vs_oracle(align, band):
+    _run(ALIGN, SA_ALIGN=align, SA_BAND=band)
 
 
 def _run(script, **env):
