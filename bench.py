@@ -209,31 +209,6 @@ class Chunked:
         return res
 
 
-def cu_split_streams(torch, device, k):
-    """Two HIP streams with complementary CU masks (hipExtStreamCreateWithCUMask): k CUs (k a
-    multiple of 8, at most 32) for the second, spread over the 8 XCDs whether the mask's bits map to
-    XCDs in blocks of 32 or interleaved (bit 32 x + x + 8 j: XCD x either way), the rest for the first."""
-    import ctypes
-    ncu = torch.cuda.get_device_properties(device).multi_processor_count
-    assert k % 8 == 0 and 0 < k <= 32 and ncu % 32 == 0, (k, ncu)
-    tb = [0] * (ncu // 32)
-    for x in range(8):
-        for j in range(k // 8):
-            bit = 32 * x + x + 8 * j
-            tb[bit // 32] |= 1 << (bit % 32)
-    fill = [~w & 0xFFFFFFFF for w in tb]
-    hip = ctypes.CDLL("libamdhip64.so")
-    torch.cuda.set_device(device)
-    out = []
-    for mask in (fill, tb):
-        st = ctypes.c_void_p()
-        arr = (ctypes.c_uint32 * len(mask))(*mask)
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), len(mask), arr)
-        assert rc == 0, rc
-        out.append(torch.cuda.ExternalStream(st.value, device=device))
-    return out
-
-
 class Pipelined:
     """--workload batch, one rank: two copies of the rank's plans (the same pairs, each with its own
     direction planes) so that batch steps overlap two deep. Step k fills copy k % 2 on the fill stream
@@ -246,10 +221,6 @@ class Pipelined:
         self.sets, self.torch = [a, b], torch
         self.s_fill = torch.cuda.current_stream(local)
         self.s_tb = torch.cuda.Stream(local)
-        tb_cus = int(os.environ.get("SA_BENCH_TB_CUS", "0"))
-        if tb_cus > 0:
-            # experiment: the traceback on tb_cus CUs of its own (stream CU masks), the fill on the rest
-            self.s_fill, self.s_tb = cu_split_streams(torch, local, tb_cus)
         self.fill_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.tb_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.k, self.pending = 0, None
