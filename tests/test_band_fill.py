@@ -115,6 +115,9 @@ cases = [(3001, 1100, 5), (2998, 700, 0), (1283, 1500, 3), (4099, 257, 5), (515,
 for k, (n, m, gap) in enumerate(cases):
     for mode in (0, 1):
         check(mode, n, m, gap, 1200 + 10 * k, k % 2 == 1, S=B50 if k % 2 == 0 else B62)
+for k, (n, m) in enumerate([(1, 300), (3, 65), (17, 200), (33, 129), (64, 700)]):  # short texts: padding reads
+    for mode in (0, 1):
+        check(mode, n, m, 5, 1400 + 10 * k, False, S=B50)
 check(0, 2500, 900, 5, 1300, True)  # DNA (copy-0 reads only with SA_ALIGN=2)
 check(1, 2047, 1300, 5, 1310, False)
 print("BAND_OK" if not bad else "BAND_BAD %r" % (bad,))
