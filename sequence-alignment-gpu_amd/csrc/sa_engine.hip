@@ -213,6 +213,7 @@ struct Knobs {
                                     // capacity (default kBandPersistRows*)
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
     int tb_cap = 0;                 // SA_TB_CAP: column-walk waves at most (0: one per pair)
+    bool tb_wide = true;            // SA_TB_WIDE=0: strip tables always 512 threads per strip
     int align = 1;                  // SA_ALIGN=0: chains of alphabets larger than 4 read the four
                                     // byte copies of their text profiles (kArr8) instead of copy 0
                                     // shifted in registers (kArr8A); 2: every alphabet (experiments)
@@ -244,6 +245,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_BAND_ROWS")) v.band_rows = std::max(0LL, std::atoll(e));
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
         if (const char *e = get("SA_TB_CAP")) v.tb_cap = std::max(0, std::atoi(e));
+        if (const char *e = get("SA_TB_WIDE")) v.tb_wide = std::atoi(e) != 0;
         if (const char *e = get("SA_ALIGN")) v.align = std::min(2, std::max(0, std::atoi(e)));
         return v;
     }();
@@ -1280,7 +1282,9 @@ int sa_plan_traceback(sa_plan *pl, void *stream)
         t.strict = kn.tb_strict ? 1 : 0;
         t.round = 1;
         w.tb_pg = pl->d_tbpg;
-        launch_tb(t, w, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, rounds, st);
+        // strip tables of 1024 threads when every strip has a CU of its own (SA_TB_WIDE=0: always 512)
+        const bool wide = knobs().tb_wide && (int)pl->strips.size() <= pl->num_cu;
+        launch_tb(t, w, (int)pl->strips.size(), (int)pl->tb_groups.size(), np, rounds, wide, st);
         HIP_TRY(hipGetLastError());
         if (kn.tb_table_timing)
         {

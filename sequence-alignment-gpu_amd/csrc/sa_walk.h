@@ -130,7 +130,8 @@ __host__ __device__ inline int tb_window_lo(int b, int n, int i0, int ra, int xa
 }
 // the table traceback of a plan's pairs with groups; the pairs it leaves are walked by tb_finish_kernel
 // with the row walk (w), so walk_rw_kernel need only run for pairs without groups
-void launch_tb(const TbArgs &a, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, hipStream_t st);
+// wide: 1024 threads per strip table instead of 512 (plans with at most one strip per CU)
+void launch_tb(const TbArgs &a, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, bool wide, hipStream_t st);
 
 struct ExpandArgs {
     const int8_t *text, *pattern;

@@ -1272,8 +1272,11 @@ __device__ __forceinline__ bool tb_pair_start(const TbArgs &a, int p, const Pair
 // strip's last down to its first. Chains that meet stay merged, so after 4 and after 16 rows the
 // distinct ones are compacted (2048 -> ~500 -> ~230 at 32768^2 random DNA) and only those walk on.
 constexpr int kTbPhases = 3;
-constexpr int kTbThreads = 512;
-__global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
+// T threads per strip: 512 lets two strips share a CU (plans with more strips than CUs); 1024 when
+// every strip has a CU of its own, where a block's serial work is the kernel's time (the first
+// phase's 2048 chains at two per thread instead of four, the staging at twice the loads in flight)
+template <int T>
+__global__ __launch_bounds__(T) void tb_table_kernel(TbArgs a)
 {
     __shared__ uint32_t nlm[kWave * kTbRow], dgm[kWave * kTbRow], nzm[kWave * kTbNz];
     __shared__ int cur[kTbK];
@@ -1397,7 +1400,7 @@ __global__ __launch_bounds__(kTbThreads) void tb_table_kernel(TbArgs a)
         __syncthreads();
         if (dbg) stamp[1 + 3 * ph] = __builtin_amdgcn_s_memrealtime();
         if (k < 0) break;
-        D = tb_compact<kTbK / kTbThreads>(cur, map, tmp, wsum, D);
+        D = tb_compact<kTbK / T>(cur, map, tmp, wsum, D);
         if (dbg)
         {
             stamp[2 + 3 * ph] = __builtin_amdgcn_s_memrealtime();
@@ -1993,14 +1996,15 @@ void launch_walk(int R, bool local, const WalkArgs &a, int np, hipStream_t st)
     else launch_walk_m<false>(R, a, np, st);
 }
 
-void launch_tb(const TbArgs &args, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, hipStream_t st)
+void launch_tb(const TbArgs &args, const WalkArgs &w, int nstrips, int ngroups, int np, int rounds, bool wide, hipStream_t st)
 {
     TbArgs a = args;
     for (int r = 1; r <= rounds; ++r)
     {
         a.round = r;
         a.last_round = r == rounds;
-        hipLaunchKernelGGL(tb_table_kernel, dim3(nstrips), dim3(kTbThreads), 0, st, a);
+        if (wide) hipLaunchKernelGGL(tb_table_kernel<1024>, dim3(nstrips), dim3(1024), 0, st, a);
+        else hipLaunchKernelGGL(tb_table_kernel<512>, dim3(nstrips), dim3(512), 0, st, a);
         hipLaunchKernelGGL(tb_compose_kernel, dim3(ngroups), dim3(1024), 0, st, a);
         hipLaunchKernelGGL(tb_resolve_kernel, dim3(np), dim3(1024), 0, st, a);
     }
