@@ -214,6 +214,7 @@ struct Knobs {
     int pair_chain_r = 0;           // SA_PAIR_CHAIN_R: rows per lane of small batches' pair-packed chains (4 / 8)
     int tb_cap = 0;                 // SA_TB_CAP: column-walk waves at most (0: one per pair)
     bool tb_wide = true;            // SA_TB_WIDE=0: strip tables always 512 threads per strip
+    bool stage_kernel = true;       // SA_STAGE_KERNEL=0: one-shot calls stage through DMA copies
     int align = 1;                  // SA_ALIGN=0: chains of alphabets larger than 4 read the four
                                     // byte copies of their text profiles (kArr8) instead of copy 0
                                     // shifted in registers (kArr8A); 2: every alphabet (experiments)
@@ -246,6 +247,7 @@ const Knobs &knobs()
         if (const char *e = get("SA_PAIR_CHAIN_R")) v.pair_chain_r = std::atoi(e) == 4 ? 4 : 8;
         if (const char *e = get("SA_TB_CAP")) v.tb_cap = std::max(0, std::atoi(e));
         if (const char *e = get("SA_TB_WIDE")) v.tb_wide = std::atoi(e) != 0;
+        if (const char *e = get("SA_STAGE_KERNEL")) v.stage_kernel = std::atoi(e) != 0;
         if (const char *e = get("SA_ALIGN")) v.align = std::min(2, std::max(0, std::atoi(e)));
         return v;
     }();
@@ -507,6 +509,7 @@ struct DeviceCtx {
     // pinned host staging: a call's uploads leave in one DMA copy and its results come back in one
     // (pageable copies go through the runtime's staging blits, ~20 us each)
     char *pinned = nullptr;
+    char *pinned_dev = nullptr;  // the same buffer as the kernels address it (stage_copy_kernel)
     size_t pinned_bytes = 0;
     // granules live in a buffer of their own (zeroed when allocated, never used for anything else)
     // and carry epochs that only grow across calls: a granule left by an earlier call never
@@ -638,8 +641,32 @@ int ctx_pinned(DeviceCtx *c, size_t bytes)
     }
     const size_t want = std::max(bytes, (size_t)1 << 20);
     HIP_TRY(hipHostMalloc((void **)&c->pinned, want, hipHostMallocDefault));
+    HIP_TRY(hipHostGetDevicePointer((void **)&c->pinned_dev, c->pinned, 0));
     c->pinned_bytes = want;
     return SA_OK;
+}
+
+// One-shot calls move their staging blob through the pinned buffer with a kernel on the call's
+// stream instead of a DMA copy: the copy engine's hand-off to and from the compute queue cost ≈ 10 us
+// each way per call (rocprofv3 memory-copy trace of the latency mode, profiles/r06/latency_*), the
+// kernel reads or writes the host buffer directly over the fabric. 16-byte vector loads and stores;
+// the last bytes one at a time. (SA_STAGE_KERNEL=0: the DMA copies.)
+__global__ __launch_bounds__(256) void stage_copy_kernel(char *dst, const char *src, uint64_t bytes)
+{
+    const uint64_t n16 = bytes / 16;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+    if (blockIdx.x == 0 && threadIdx.x < bytes % 16) dst[16 * n16 + threadIdx.x] = src[16 * n16 + threadIdx.x];
+}
+
+hipError_t stage_copy(char *dst, const char *src, size_t bytes, hipStream_t st)
+{
+    if (!bytes) return hipSuccess;
+    const uint64_t n16 = bytes / 16 + 1;
+    const int grid = (int)std::min<uint64_t>(1024, (n16 + 255) / 256);
+    hipLaunchKernelGGL(stage_copy_kernel, dim3(grid), dim3(256), 0, st, dst, src, (uint64_t)bytes);
+    return hipGetLastError();
 }
 
 constexpr size_t kArenaAlign = 256;
@@ -1004,7 +1031,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
         put(pl->d_ws_text, in->text, inN);
         put(pl->d_ws_pattern, in->pattern, inM);
         std::memset(h + ((char *)pl->d_ctrl - pl->d_up), 0, sizeof(Control));
-        if (hipMemcpyAsync(pl->d_up, h, pl->up_bytes, hipMemcpyHostToDevice, pl->own) != hipSuccess)
+        if ((knobs().stage_kernel ? stage_copy(pl->d_up, ws->pinned_dev, pl->up_bytes, pl->own)
+                                  : hipMemcpyAsync(pl->d_up, h, pl->up_bytes, hipMemcpyHostToDevice, pl->own)) != hipSuccess)
         {
             free_plan(pl);
             restore();
@@ -1541,7 +1569,8 @@ int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *
     if (!fillOnly && (rc = sa_plan_traceback(pl, st))) return rc;
     // [ctrl | result | out_text | out_pattern]; fill-only needs the control word alone
     const size_t dn = fillOnly ? sizeof(Control) : pl->dn_bytes;
-    HIP_TRY(hipMemcpyAsync(ws->pinned, pl->d_dn, dn, hipMemcpyDeviceToHost, st));
+    if (knobs().stage_kernel) HIP_TRY(stage_copy(ws->pinned_dev, pl->d_dn, dn, st));
+    else HIP_TRY(hipMemcpyAsync(ws->pinned, pl->d_dn, dn, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const char *h = ws->pinned;
     Control ctrl;
