@@ -221,6 +221,9 @@ class Pipelined:
         self.sets, self.torch = [a, b], torch
         self.s_fill = torch.cuda.current_stream(local)
         self.s_tb = torch.cuda.Stream(local)
+        if os.environ.get("SA_BENCH_FILL_PRIO", "0") != "0":
+            # experiment: the fill stream (encode + fill) at high priority, the traceback at normal
+            self.s_fill = torch.cuda.Stream(local, priority=-1)
         self.fill_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.tb_done = [torch.cuda.Event(), torch.cuda.Event()]
         self.k, self.pending = 0, None
