@@ -33,8 +33,16 @@ namespace sa {
 //   kArr            A dword arrays of code_len: array a holds table[a][t[x]] at kPad + x;
 //   kArr8           4A byte arrays of code_len bytes: copy (a, r) holds table[a][t[x]] at kPad + x + r.
 __global__ void encode_text_kernel(const int8_t *text, const int8_t *pattern, const PairDesc *pairs, int32_t *codes,
-                                   int A, int SK, const int32_t *table, Control *ctrl)
+                                   int A, int SK, const int32_t *table, Control *ctrl, uint32_t epoch)
 {
+    // the fill's control word starts here (no memset launch before each fill): the queues and the
+    // abort flag at zero; bad_input carries the epoch of the fill it reports, so it needs no reset
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    {
+        ctrl->queue_head = 0;
+        ctrl->band_head = 0;
+        ctrl->abort_flag = 0;
+    }
     const PairDesc pd = pairs[blockIdx.y];
     // the arenas must hold alphabet indices 0..A-1 (Request::textBytes / patternBytes are indices,
     // utilities.cpp:52); the kernels clamp, so a bad byte is reported instead of aligned silently
@@ -51,7 +59,7 @@ __global__ void encode_text_kernel(const int8_t *text, const int8_t *pattern, co
         const int c = text[pd.text_off + x];
         bad = bad || c < 0 || c >= A;
     }
-    if (bad) __hip_atomic_store(&ctrl->bad_input, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bad) __hip_atomic_store(&ctrl->bad_input, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (SK == kPair)
     {
         // selectors of pairs (2q, 2q+1) in pair 2q's block, padding included (0x0c0c0c0c = zeros)
@@ -1054,7 +1062,8 @@ int plan_create(const sa_params *P, const sa_pair *pairs, int64_t np, int device
                hipMemcpyAsync(pl->d_prof, prof.data(), sizeof(int32_t) * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemcpyAsync(pl->d_table, table.data(), sizeof(int32_t) * A * A, hipMemcpyHostToDevice, st) == hipSuccess &&
                hipMemsetAsync(pl->d_bnd, 0, bndB, st) == hipSuccess &&
-               hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess;
+               hipMemsetAsync(pl->d_best, 0, bestB, st) == hipSuccess &&
+               hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st) == hipSuccess;  // (bad_input: no stale epoch)
     // expansion flags carry the plan's epoch, which starts again at 1 for a plan of its own: a freed
     // plan's flags at the same address would match (workspace plans draw epochs from their device's
     // context, which only grow, so their arena needs no clearing)
@@ -1094,7 +1103,11 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
     uint32_t *es = pl->epoch_src ? pl->epoch_src : &pl->epoch;
     if (++*es == 0) ++*es;
     pl->epoch = *es;
-    if (!pl->ctrl_ready) HIP_TRY(hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st));
+    // A plan of one pair leaves the reset of its control word to the encode kernel below; plans of
+    // several pairs keep the memset launch: without it the pipelined batch step (two plans, the fill
+    // and the traceback on two streams) went from 2.45 to 3.34 ms, while the same reset with the
+    // launch kept measured 2.45 (profiles/r06/ab_ctrl_reset_diagnosis_v1.log)
+    if (!pl->ctrl_ready && pl->pairs.size() != 1) HIP_TRY(hipMemsetAsync(pl->d_ctrl, 0, sizeof(Control), st));
     pl->ctrl_ready = false;
     const int np = (int)pl->pairs.size();
     if (np > 0)
@@ -1112,7 +1125,7 @@ int sa_plan_fill(sa_plan *pl, const void *d_text, const void *d_pattern, void *s
             const int cnt = std::min(65534, np - y0);  // even: kPair pairs (2q, 2q+1) stay in one launch
             hipLaunchKernelGGL(encode_text_kernel, dim3(gx, cnt), dim3(256), 0, st, (const int8_t *)d_text,
                                (const int8_t *)d_pattern, pl->d_pairs + y0, pl->d_codes, pl->A, pl->sk, pl->d_table,
-                               pl->d_ctrl);
+                               pl->d_ctrl, pl->epoch);
         }
         HIP_TRY(hipGetLastError());
         if (int rc = debug_sync(st, "encode_text_kernel")) return rc;
@@ -1376,7 +1389,7 @@ int sa_plan_fetch_results(sa_plan *pl, sa_result *out, void *stream)
     if (out && !pl->pairs.empty())
         HIP_TRY(hipMemcpyAsync(out, pl->d_results, sizeof(sa_result) * pl->pairs.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
+    if (ctrl.bad_input == pl->epoch) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     return SA_OK;
 }
@@ -1419,7 +1432,7 @@ int sa_plan_fetch_all(sa_plan *pl, sa_result *out, char *tb, char *pb, uint64_t 
     if (pb && pl->out_bytes) HIP_TRY(hipMemcpyAsync(pb, pl->d_out_pattern, pl->out_bytes, hipMemcpyDeviceToHost, st));
     for (size_t i = 0; i < pl->pairs.size(); ++i) offsets[i] = pl->pairs[i].out_off;
     HIP_TRY(hipStreamSynchronize(st));
-    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
+    if (ctrl.bad_input == pl->epoch) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     return SA_OK;
 }
@@ -1576,7 +1589,7 @@ int sa_align_pair(const sa_params *P, const char *text, uint64_t n, const char *
     Control ctrl;
     std::memcpy(&ctrl, h, sizeof(Control));
     // also in fill-only mode: a fill whose hand-off timed out produced garbage, not a fill time
-    if (ctrl.bad_input) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
+    if (ctrl.bad_input == pl->epoch) return fail(SA_ERR_INVALID, "a text or pattern byte is outside the alphabet (0..A-1)");
     if (ctrl.abort_flag) return fail(SA_ERR_TIMEOUT, "fill aborted: a strip hand-off timed out");
     if (!fillOnly)
     {

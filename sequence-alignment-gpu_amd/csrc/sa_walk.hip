@@ -1964,7 +1964,7 @@ __global__ __launch_bounds__(kExpThreads) void expand_kernel(ExpandArgs a)
         // the control word of this fill: a pair aligned after a hand-off timeout or on bad input carries
         // the error itself, so a device-to-device copy of the results (sa_plan_copy_results, the RCCL
         // gather) keeps it
-        r.status = a.ctrl->abort_flag || h.err ? SA_ERR_TIMEOUT : (a.ctrl->bad_input ? SA_ERR_INVALID : SA_OK);
+        r.status = a.ctrl->abort_flag || h.err ? SA_ERR_TIMEOUT : (a.ctrl->bad_input == a.epoch ? SA_ERR_INVALID : SA_OK);
         r.num_alignment_bytes = (uint64_t)L;
         r.start_text = (uint64_t)h.start_text;
         r.start_pattern = (uint64_t)h.start_pattern;
